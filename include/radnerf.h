@@ -1,0 +1,171 @@
+/*
+ * radnerf.h — C ABI of librn.so, the MI355X (gfx950) Rad-NeRF hot path.
+ *
+ * Every entry point takes plain device pointers + sizes + a hipStream_t passed
+ * as `void*`, launches asynchronously on that stream and returns
+ *   0 = ok, 1 = invalid argument, 2 = launch failure
+ * (rn_last_error() returns a thread-local message).  No torch types appear in
+ * any signature.  Each function cites the reference interface it replaces
+ * (paths relative to thu-nics/Rad-NeRF).  The Python binding that mirrors the
+ * reference's `vren` module lives in rad-nerf_amd/radnerf_amd/vren.py; see
+ * INTEGRATION.md for the ctypes/pybind stubs a maintainer would add.
+ */
+#ifndef RADNERF_H
+#define RADNERF_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int rn_version(void);
+const char* rn_last_error(void);
+
+/* ---- ray / AABB -----------------------------------------------------------
+ * replaces vren.ray_aabb_intersect  (models/csrc/binding.cpp:4-16,
+ * intersection.cu:25-100).  hits_t (n_rays, max_hits, 2), hits_voxel_idx
+ * (n_rays, max_hits) are fully written (-1 = no hit).                       */
+int rn_ray_aabb_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                          const float* half_sizes, int64_t n_rays, int64_t n_voxels,
+                          int32_t max_hits, int32_t* hit_cnt, float* hits_t,
+                          int64_t* hits_voxel_idx, void* stream);
+
+/* ---- training ray march ----------------------------------------------------
+ * replaces vren.raymarching_train (binding.cpp:60-81, raymarching.cu:166-332)
+ * as three deterministic steps: count -> rn_scan_segments -> write.
+ * hits_t is the (n_rays, 2) near/far slice, noise (n_rays) in [0,1).       */
+int rn_raymarching_train_count(const float* rays_o, const float* rays_d, const float* hits_t,
+                               const uint8_t* density_bitfield, int32_t cascades, float scale,
+                               float exp_step_factor, const float* noise, int32_t grid_size,
+                               int32_t max_samples, int64_t n_rays, int32_t* counts,
+                               void* stream);
+int rn_raymarching_train_write(const float* rays_o, const float* rays_d, const float* hits_t,
+                               const uint8_t* density_bitfield, int32_t cascades, float scale,
+                               float exp_step_factor, const float* noise, int32_t grid_size,
+                               int32_t max_samples, int64_t n_rays, const int32_t* counts,
+                               const int32_t* offsets, int64_t* rays_a, float* xyzs, float* dirs,
+                               float* deltas, float* ts, void* stream);
+
+/* exclusive scan of counts[n_seg][n_per]; segment k starts at an `align`
+ * multiple: seg_base[k], seg_count[k]; meta[0] = aligned end, meta[1] = total.
+ * (replaces the atomicAdd slot allocation of raymarching.cu:237-238)         */
+int rn_scan_segments(const int32_t* counts, int32_t n_seg, int64_t n_per, int32_t align,
+                     int32_t* offsets, int32_t* seg_base, int32_t* seg_count, int32_t* meta,
+                     void* stream);
+
+/* ---- test-time march -------------------------------------------------------
+ * replaces vren.raymarching_test (binding.cpp:84-106, raymarching.cu:335-454);
+ * hits_t (n_rays_total, 2) is advanced in place.                            */
+int rn_raymarching_test(const float* rays_o, const float* rays_d, float* hits_t,
+                        const int64_t* alive_indices, int64_t n_alive,
+                        const uint8_t* density_bitfield, int32_t cascades, float scale,
+                        float exp_step_factor, int32_t grid_size, int32_t max_samples,
+                        int32_t n_samples, float* xyzs, float* dirs, float* deltas, float* ts,
+                        int32_t* n_eff_samples, void* stream);
+
+/* ---- fused multi-sub-NeRF march (ml_rendering.py:47-52 + :174-179) -------
+ * AABB + NEAR clamp + jitter + march for K models in one launch; counts and
+ * noise are [K][n_rays]; writes compact samples (t, dt, ray).               */
+int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* center,
+                      const float* half_size, float near_distance, const float* noise,
+                      const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
+                      int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
+                      int32_t max_samples, int64_t n_rays, int32_t* counts, void* stream);
+int rn_ml_march_write(const float* rays_o, const float* rays_d, const float* center,
+                      const float* half_size, float near_distance, const float* noise,
+                      const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
+                      int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
+                      int32_t max_samples, int64_t n_rays, const int32_t* counts,
+                      const int32_t* offsets, float* ts, float* deltas, int32_t* ray_of,
+                      void* stream);
+
+/* ---- compositing -----------------------------------------------------------
+ * replaces vren.composite_train_fw / _bw / composite_test_fw
+ * (binding.cpp:109-194, volumerendering.cu:6-286).                          */
+int rn_composite_train_fw(const float* sigmas, const float* rgbs, const float* deltas,
+                          const float* ts, const int64_t* rays_a, int64_t n_rows,
+                          float T_threshold, int64_t* total_samples, float* opacity,
+                          float* depth, float* rgb, float* ws, void* stream);
+int rn_composite_train_bw(const float* dL_dopacity, const float* dL_ddepth, const float* dL_drgb,
+                          const float* dL_dws, const float* sigmas, const float* rgbs,
+                          const float* ws, const float* deltas, const float* ts,
+                          const int64_t* rays_a, int64_t n_rows, const float* opacity,
+                          const float* depth, const float* rgb, float T_threshold,
+                          float* dL_dsigmas, float* dL_drgbs, void* stream);
+int rn_composite_test_fw(const float* sigmas, const float* rgbs, const float* deltas,
+                         const float* ts, int64_t n_alive, int32_t n_samples,
+                         int64_t* alive_indices, float T_threshold, const int32_t* n_eff_samples,
+                         float* opacity, float* depth, float* rgb, void* stream);
+
+/* fused ml path: per-(model, ray) composite + gated combine
+ * (ml_rendering.py:41-78 and the bg term of :192-200)                       */
+int rn_ml_composite_fw(const float* sigmas, const float* rgbs, const float* deltas,
+                       const float* ts, const int32_t* counts, const int32_t* offsets,
+                       int64_t n_rays, int32_t n_models, float T_threshold, int32_t* used,
+                       float* opacity_k, float* depth_k, float* rgb_k, float* ws, void* stream);
+int rn_ml_combine_fw(const float* gate, const float* opacity_k, const float* depth_k,
+                     const float* rgb_k, const float* bg, int64_t n_rays, int32_t n_models,
+                     float* rgb, float* opacity, float* depth, void* stream);
+int rn_ml_combine_bw(const float* dL_drgb, const float* dL_dopacity, const float* opacity_k,
+                     const float* rgb_k, const float* bg, int64_t n_rays, int32_t n_models,
+                     float* dL_dgate, void* stream);
+int rn_ml_composite_bw(const float* dL_drgb, const float* dL_dopacity, const float* dL_ddepth,
+                       const float* gate, const float* bg, const float* sigmas,
+                       const float* rgbs, const float* deltas, const float* ts,
+                       const int32_t* counts, const int32_t* offsets, const float* opacity_k,
+                       const float* depth_k, const float* rgb_k, int64_t n_rays,
+                       int32_t n_models, float T_threshold, float* dL_dsigmas, float* dL_drgbs,
+                       void* stream);
+
+/* ---- field: shared hash grid + per-model geo/rgb MLP -----------------------
+ * replaces MNGP.forward / tcnn Encoding+Network fwd/bwd
+ * (models/networks.py:229-328, custom_functions.py:162-173).
+ * Sample input: xyzs/dirs (n_samples, 3) [single model], or, when xyzs is
+ * NULL, compact (ts, ray_of) + rays with per-model seg_base/seg_count.
+ * level_* (16 entries) and xyz_min/extent (3) are HOST arrays read at launch;
+ * frags = packed f16 weights (device), dw_map = layout.field_dw_map().      */
+int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
+                 const int32_t* ray_of, const float* rays_o, const float* rays_d,
+                 const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
+                 const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
+                 const uint32_t* level_res, const float* level_scale, const float* xyz_min,
+                 const float* extent, const void* frags, float* sigma, float* rgb,
+                 int32_t blocks_per_model, void* stream);
+int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
+                 const int32_t* ray_of, const float* rays_o, const float* rays_d,
+                 const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
+                 const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
+                 const uint32_t* level_res, const float* level_scale, const float* xyz_min,
+                 const float* extent, const void* frags, const int16_t* dw_map,
+                 const float* dL_dsigma, const float* dL_drgb, float* grid_grad, float* dw,
+                 int32_t blocks_per_model, void* stream);
+
+/* ---- ray gate (networks.py:1070-1093) --------------------------------------
+ * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)
+ * as (x, x+3, 6) or rays_o/rays_d as (rays_o, rays_d, 3).  importance (K) is
+ * accumulated (zero it first) = gate.sum(0).                                */
+int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
+                int32_t n_models, const void* frags, float* gate, float* importance,
+                int32_t n_blocks, void* stream);
+int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
+                int32_t n_models, const void* frags, const int16_t* dw_map,
+                const float* dL_dgate, float* dw, int32_t n_params, int32_t n_blocks,
+                void* stream);
+
+/* ---- parameter packing (f32 master -> f16 MFMA fragments / f16 grid) ------*/
+int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,
+                int32_t n_models, int64_t dst_stride, void* dst, void* stream);
+int rn_to_f16(const float* src, int64_t n, void* dst, void* stream);
+
+/* ---- occupancy grid maintenance (raymarching.cu:62-161, "next" row) -------*/
+int rn_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream);
+int rn_morton3d_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
+int rn_packbits(const float* density_grid, int64_t n_bytes, float density_threshold,
+                uint8_t* density_bitfield, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RADNERF_H */

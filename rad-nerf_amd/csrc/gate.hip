@@ -1,0 +1,278 @@
+// Ray gate of Rad-NeRF on gfx950: MLP 6 -> 64 -> 64 -> 64 -> 64 -> K (ReLU,
+// no bias, f16 like tcnn FullyFusedMLP) + softmax, forward and backward.
+//
+// Reference: models/networks.py:1070-1093 (Ray_Gate), call site
+// models/ml_rendering.py:31-36 (input cat(rays_o, rays_d) or cat(rays_o, imgs_d)).
+// Same MFMA orientation and fragment conventions as field.hip (rn_mlp.h).
+#include "rn_mlp.h"
+#pragma clang fp contract(off)
+
+#define GATE_FWD_FRAGS 30
+#define GATE_FRAGS 56
+#define GATE_DW_TILES 16
+#define GATE_WAVES 4
+#define GATE_MAX_PARAMS (12672 + 64 * 16)
+
+struct GateArgs {
+    const float* in0; const float* in1;         // input cols 0..2 / 3..5, row stride `stride`
+    int stride;
+    int64_t n_rays; int K;
+    const rn_half* frags;                        // [GATE_FRAGS][512]
+    const int16_t* dwmap;                        // [GATE_DW_TILES][16][64]
+    float* gate;                                 // (B,K) softmax
+    float* importance;                           // (K) gate.sum(0), may be null
+    const float* dgate;                          // (B,K) dL/dgate
+    float* dw;                                   // (n_params)
+    int n_params;
+};
+
+namespace {
+
+struct GateState { half8 x; half8 h[4][4]; f32x16 logit; };
+
+__device__ __forceinline__ void gate_input(const GateArgs& a, int64_t r, bool valid, half8& x) {
+    const int lane = rn_lane(), h = lane >> 5;
+    x = rn_zero8();
+    if (!valid) return;
+    // element j <-> input 8(j>>2) + 4h + (j&3); inputs 0..5 = (o, d)
+    const float* p0 = a.in0 + r * a.stride;
+    const float* p1 = a.in1 + r * a.stride;
+    if (h == 0) {
+        x[0] = (rn_half)p0[0]; x[1] = (rn_half)p0[1]; x[2] = (rn_half)p0[2]; x[3] = (rn_half)p1[0];
+    } else {
+        x[0] = (rn_half)p1[1]; x[1] = (rn_half)p1[2];
+    }
+}
+
+__device__ __forceinline__ void gate_forward(const rn_half* W, GateState& st) {
+    f32x16 a0 = rn_zero16(), a1 = rn_zero16();
+    a0 = rn_mfma(rn_frag(W, 0), st.x, a0);
+    a1 = rn_mfma(rn_frag(W, 1), st.x, a1);
+    rn_acc_to_frags<true>(a0, st.h[0][0], st.h[0][1]);
+    rn_acc_to_frags<true>(a1, st.h[0][2], st.h[0][3]);
+#pragma unroll
+    for (int L = 1; L < 4; ++L) {
+        a0 = rn_zero16(); a1 = rn_zero16();
+        const int fb = 2 + 8 * (L - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            a0 = rn_mfma(rn_frag(W, fb + q), st.h[L - 1][q], a0);
+            a1 = rn_mfma(rn_frag(W, fb + 4 + q), st.h[L - 1][q], a1);
+        }
+        rn_acc_to_frags<true>(a0, st.h[L][0], st.h[L][1]);
+        rn_acc_to_frags<true>(a1, st.h[L][2], st.h[L][3]);
+    }
+    st.logit = rn_zero16();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) st.logit = rn_mfma(rn_frag(W, 26 + q), st.h[3][q], st.logit);
+}
+
+// softmax over the K logit rows of this lane's sample (rows spread over the
+// two lane halves: reg i <-> row (i&3) + 8(i>>2) + 4h).  Returns probs in the
+// same register positions (0 for rows >= K).
+__device__ __forceinline__ f32x16 gate_softmax(const f32x16& logit, int K) {
+    const int h = rn_lane() >> 5;
+    float z[16];
+    float m = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        z[i] = (float)(rn_half)logit[i];   // tcnn f16 output, softmax in f32
+        if (row < K) m = fmaxf(m, z[i]);
+    }
+    m = fmaxf(m, __shfl_xor(m, 32));
+    float sum = 0.f;
+    float e[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        e[i] = row < K ? expf(z[i] - m) : 0.f;
+        sum += e[i];
+    }
+    sum += __shfl_xor(sum, 32);
+    f32x16 p;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) p[i] = e[i] / sum;
+    return p;
+}
+
+__global__ void __launch_bounds__(GATE_WAVES * 64)
+k_gate_fwd(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) rn_half sW[GATE_FWD_FRAGS * RN_FRAG_HALFS];
+    rn_block_copy16(sW, a.frags, GATE_FWD_FRAGS * RN_FRAG_BYTES);
+    __syncthreads();
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    const int64_t n_tiles = (a.n_rays + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * GATE_WAVES + threadIdx.x / RN_WAVE; tile < n_tiles;
+         tile += (int64_t)gridDim.x * GATE_WAVES) {
+        const int64_t r = tile * 32 + c;
+        const bool valid = r < a.n_rays;
+        GateState st;
+        gate_input(a, r, valid, st.x);
+        gate_forward(sW, st);
+        const f32x16 p = gate_softmax(st.logit, a.K);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (row < a.K) {
+                if (valid) a.gate[r * a.K + row] = p[i];
+                if (a.importance) {
+                    // per-wave column sum over the 32 samples of this half
+                    float v = valid ? p[i] : 0.f;
+#pragma unroll
+                    for (int off = 16; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                    if (c == 0) atomicAdd(&a.importance[row], v);
+                }
+            }
+        }
+    }
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+#define GSTG_HALFS (64 * RN_STG_STRIDE)
+
+__global__ void __launch_bounds__(GATE_WAVES * 64)
+k_gate_bwd(GateArgs a) {
+    __shared__ __attribute__((aligned(16))) rn_half sW[GATE_FRAGS * RN_FRAG_HALFS];
+    __shared__ __attribute__((aligned(16))) rn_half sStg[GATE_WAVES * GSTG_HALFS];
+    __shared__ __attribute__((aligned(16))) float sDW[GATE_MAX_PARAMS];
+    rn_block_copy16(sW, a.frags, GATE_FRAGS * RN_FRAG_BYTES);
+    for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) sDW[i] = 0.f;
+    __syncthreads();
+    const int wid = threadIdx.x / RN_WAVE;
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    rn_half* stg = sStg + wid * GSTG_HALFS;
+    const half8 z8 = rn_zero8();
+    const int64_t n_tiles = (a.n_rays + 31) / 32;
+    for (int64_t tile = (int64_t)blockIdx.x * GATE_WAVES + wid; tile < n_tiles;
+         tile += (int64_t)gridDim.x * GATE_WAVES) {
+        const int64_t r = tile * 32 + c;
+        const bool valid = r < a.n_rays;
+        GateState st;
+        gate_input(a, r, valid, st.x);
+        gate_forward(sW, st);
+        const f32x16 p = gate_softmax(st.logit, a.K);
+        // softmax backward: dz = p * (dg - sum_j p_j dg_j)
+        float dg[16];
+        float dot = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+            dg[i] = (valid && row < a.K) ? a.dgate[r * a.K + row] : 0.f;
+            dot += p[i] * dg[i];
+        }
+        dot += __shfl_xor(dot, 32);
+        f32x16 dz;
+        float dmax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { dz[i] = p[i] * (dg[i] - dot); dmax = fmaxf(dmax, fabsf(dz[i])); }
+        const float gscale = rn_wave_grad_scale(dmax);
+        const float ginv = 1.0f / gscale;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dz[i] *= gscale;
+        half8 dz0, dz1;
+        rn_acc_to_frags<false>(dz, dz0, dz1);   // rows 0..15 in dz0 (K <= 16)
+        // dH3 = W4^T dz ; dH2 = W3^T dH3 ; dH1 = W2^T dH2 ; dH0 = W1^T dH1
+        half8 dh[4][4];
+        {
+            f32x16 b0 = rn_zero16(), b1 = rn_zero16();
+            b0 = rn_mfma(rn_frag(sW, 30), dz0, b0);
+            b1 = rn_mfma(rn_frag(sW, 31), dz0, b1);
+            rn_acc_to_frags_masked(b0, st.h[3][0], st.h[3][1], dh[3][0], dh[3][1]);
+            rn_acc_to_frags_masked(b1, st.h[3][2], st.h[3][3], dh[3][2], dh[3][3]);
+        }
+#pragma unroll
+        for (int L = 3; L >= 1; --L) {
+            const int fb = 32 + 8 * (3 - L);
+            f32x16 b0 = rn_zero16(), b1 = rn_zero16();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                b0 = rn_mfma(rn_frag(sW, fb + q), dh[L][q], b0);
+                b1 = rn_mfma(rn_frag(sW, fb + 4 + q), dh[L][q], b1);
+            }
+            rn_acc_to_frags_masked(b0, st.h[L - 1][0], st.h[L - 1][1], dh[L - 1][0], dh[L - 1][1]);
+            rn_acc_to_frags_masked(b1, st.h[L - 1][2], st.h[L - 1][3], dh[L - 1][2], dh[L - 1][3]);
+        }
+        const int16_t* map = a.dwmap;
+        // W4: dY = dz (rows 0..15), X = H3
+        rn_stage_frag(stg, 0, 0, dz0); rn_stage_frag(stg, 0, 1, z8);
+#pragma unroll
+        for (int nn = 0; nn < 2; ++nn) {
+            rn_stage_frag(stg, 32, 0, st.h[3][2 * nn]); rn_stage_frag(stg, 32, 1, st.h[3][2 * nn + 1]);
+            wave_lds_fence();
+            rn_dw_tile(stg, 0, stg, 32, map + (14 + nn) * 1024, sDW, ginv);
+            wave_lds_fence();
+        }
+        // W1..W3: dY = dH_L, X = H_{L-1}
+#pragma unroll
+        for (int L = 1; L <= 3; ++L) {
+#pragma unroll
+            for (int m = 0; m < 2; ++m) {
+                rn_stage_frag(stg, 0, 0, dh[L][2 * m]); rn_stage_frag(stg, 0, 1, dh[L][2 * m + 1]);
+#pragma unroll
+                for (int nn = 0; nn < 2; ++nn) {
+                    rn_stage_frag(stg, 32, 0, st.h[L - 1][2 * nn]);
+                    rn_stage_frag(stg, 32, 1, st.h[L - 1][2 * nn + 1]);
+                    wave_lds_fence();
+                    rn_dw_tile(stg, 0, stg, 32, map + (2 + 4 * (L - 1) + 2 * m + nn) * 1024, sDW, ginv);
+                    wave_lds_fence();
+                }
+            }
+        }
+        // W0: dY = dH0, X = input (rows 0..15; 16..31 zero)
+        rn_stage_frag(stg, 32, 0, st.x); rn_stage_frag(stg, 32, 1, z8);
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+            rn_stage_frag(stg, 0, 0, dh[0][2 * m]); rn_stage_frag(stg, 0, 1, dh[0][2 * m + 1]);
+            wave_lds_fence();
+            rn_dw_tile(stg, 0, stg, 32, map + m * 1024, sDW, ginv);
+            wave_lds_fence();
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) {
+        const float v = sDW[i];
+        if (v != 0.f) atomicAdd(&a.dw[i], v);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays, int32_t n_models,
+                const void* frags, float* gate, float* importance, int32_t n_blocks,
+                void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && n_models <= 16 && n_blocks >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(in0 && in1 && frags && gate && stride >= 3, "null pointer / bad stride");
+    GateArgs a{};
+    a.in0 = in0; a.in1 = in1; a.stride = stride; a.n_rays = n_rays; a.K = n_models;
+    a.frags = (const rn_half*)frags; a.gate = gate; a.importance = importance;
+    k_gate_fwd<<<n_blocks, GATE_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays, int32_t n_models,
+                const void* frags, const int16_t* dw_map, const float* dL_dgate, float* dw,
+                int32_t n_params, int32_t n_blocks, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && n_models <= 16 && n_blocks >= 1, "bad sizes");
+    RN_CHECK_ARG(n_params == 12672 + 64 * n_models, "n_params mismatch");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(in0 && in1 && frags && dw_map && dL_dgate && dw && stride >= 3,
+                 "null pointer / bad stride");
+    GateArgs a{};
+    a.in0 = in0; a.in1 = in1; a.stride = stride; a.n_rays = n_rays; a.K = n_models;
+    a.frags = (const rn_half*)frags; a.dwmap = dw_map; a.dgate = dL_dgate; a.dw = dw;
+    a.n_params = n_params;
+    k_gate_bwd<<<n_blocks, GATE_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,92 @@
+// Occupancy-grid maintenance kernels + library-wide error/version plumbing.
+//
+// Reference: models/csrc/raymarching.cu:62-161 (morton3D, morton3D_invert,
+// packbits), used by MNGP.update_density_grid (models/networks.py:330-409).
+#include "rn_common.h"
+#include <stdarg.h>
+#include <stdio.h>
+#pragma clang fp contract(off)
+
+static thread_local char g_err[512] = {0};
+
+extern "C" void rn_set_error(const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+}
+
+namespace {
+
+__global__ void __launch_bounds__(256)
+k_morton3d(int64_t n, const int32_t* __restrict__ coords, int32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = (int32_t)rn_morton3d(coords[3 * i], coords[3 * i + 1], coords[3 * i + 2]);
+}
+
+__global__ void __launch_bounds__(256)
+k_morton3d_invert(int64_t n, const int32_t* __restrict__ idx, int32_t* __restrict__ coords) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t v = (uint32_t)idx[i];
+    coords[3 * i + 0] = rn_morton3d_invert(v >> 0);
+    coords[3 * i + 1] = rn_morton3d_invert(v >> 1);
+    coords[3 * i + 2] = rn_morton3d_invert(v >> 2);
+}
+
+// 16 bytes of bitfield per thread: 128 density cells read as 32 x float4
+__global__ void __launch_bounds__(256)
+k_packbits(int64_t n_bytes, const float* __restrict__ grid, float thr, uint8_t* __restrict__ bits) {
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_bytes) return;
+    const float4* g = reinterpret_cast<const float4*>(grid + 8 * b);
+    const float4 lo = g[0], hi = g[1];
+    uint8_t v = 0;
+    v |= (lo.x > thr) << 0; v |= (lo.y > thr) << 1; v |= (lo.z > thr) << 2; v |= (lo.w > thr) << 3;
+    v |= (hi.x > thr) << 4; v |= (hi.y > thr) << 5; v |= (hi.z > thr) << 6; v |= (hi.w > thr) << 7;
+    bits[b] = v;
+}
+
+inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+}  // namespace
+
+extern "C" {
+
+int rn_version(void) { return 1; }
+
+const char* rn_last_error(void) { return g_err; }
+
+int rn_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    if (n == 0) return 0;
+    RN_CHECK_ARG(coords && indices, "null pointer");
+    k_morton3d<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, coords, indices);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_morton3d_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    if (n == 0) return 0;
+    RN_CHECK_ARG(coords && indices, "null pointer");
+    k_morton3d_invert<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, indices, coords);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_packbits(const float* density_grid, int64_t n_bytes, float density_threshold,
+                uint8_t* density_bitfield, void* stream) {
+    RN_CHECK_ARG(n_bytes >= 0, "bad size");
+    if (n_bytes == 0) return 0;
+    RN_CHECK_ARG(density_grid && density_bitfield, "null pointer");
+    RN_CHECK_ARG(((uintptr_t)density_grid & 15) == 0, "density_grid must be 16-byte aligned");
+    k_packbits<<<nblk(n_bytes, 256), 256, 0, (hipStream_t)stream>>>(n_bytes, density_grid,
+                                                                     density_threshold,
+                                                                     density_bitfield);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

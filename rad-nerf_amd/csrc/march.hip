@@ -1,0 +1,479 @@
+// Occupancy-grid ray marching for gfx950.
+//
+// Reference: models/csrc/raymarching.cu:166-332 (raymarching_train_kernel),
+//            :335-454 (raymarching_test_kernel), intersection.cu:5-56 (AABB).
+//
+// Differences by design:
+//  * deterministic slot allocation: count pass -> exclusive scan -> write pass
+//    (the reference allocates with atomicAdd, so its row order is random; we
+//    emit rays_a in ray order, start = exclusive prefix of the counts);
+//  * outputs are exactly sized; no B*max_samples zero-fill;
+//  * the fused multi-sub-NeRF path marches all K sub-NeRFs in one launch,
+//    does the ray/AABB test + NEAR_DISTANCE clamp inline, and stores a compact
+//    12 B sample record (t, dt, ray) instead of 32 B (xyz, dir, t, dt):
+//    xyz is recomputed bit-identically downstream as fmaf(t, d, o).
+#include "rn_common.h"
+#pragma clang fp contract(off)
+
+namespace {
+
+struct MarchCfg {
+    int cascades;
+    int grid_size;
+    int max_samples;
+    float scale;      // used for mip_bound and (train) calc_dt
+    float dt_scale;   // `scale` argument handed to calc_dt (== cascades for test)
+    float esf;
+};
+
+struct NoSink {
+    __device__ __forceinline__ void emit(int, float, float, float, float, float) const {}
+};
+
+// xyz/dir/t/dt sink with the reference layout (raymarching.cu:265-267)
+struct RefSink {
+    float* __restrict__ xyzs; float* __restrict__ dirs;
+    float* __restrict__ ts;   float* __restrict__ deltas;
+    float dx, dy, dz;
+    __device__ __forceinline__ void emit(int s, float x, float y, float z, float t, float dt) const {
+        xyzs[3 * s + 0] = x; xyzs[3 * s + 1] = y; xyzs[3 * s + 2] = z;
+        dirs[3 * s + 0] = dx; dirs[3 * s + 1] = dy; dirs[3 * s + 2] = dz;
+        ts[s] = t; deltas[s] = dt;
+    }
+};
+
+// compact sink for the fused path: t, dt and owning ray
+struct CompactSink {
+    float* __restrict__ ts; float* __restrict__ deltas; int32_t* __restrict__ ray_of;
+    int ray;
+    __device__ __forceinline__ void emit(int s, float, float, float, float t, float dt) const {
+        ts[s] = t; deltas[s] = dt; ray_of[s] = ray;
+    }
+};
+
+// One occupancy query + step of raymarching.cu:205-233.  Returns true if the
+// cell at t is occupied; otherwise advances t past the cell exit.
+__device__ __forceinline__ bool march_step(float& t, float ox, float oy, float oz,
+                                           float dx, float dy, float dz,
+                                           float dxi, float dyi, float dzi,
+                                           const uint8_t* __restrict__ bitfield,
+                                           const MarchCfg& c, float& x, float& y,
+                                           float& z, float& dt) {
+    const uint32_t g3 = (uint32_t)c.grid_size * c.grid_size * c.grid_size;
+    const float gsi = 1.0f / c.grid_size;
+    x = fmaf(t, dx, ox); y = fmaf(t, dy, oy); z = fmaf(t, dz, oz);
+    dt = rn_calc_dt(t, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+    const int mip = max(rn_mip_from_pos(x, y, z, c.cascades),
+                        rn_mip_from_dt(dt, c.grid_size, c.cascades));
+    const float mb = fminf(scalbnf(1.0f, mip - 1), c.scale);
+    const float mbi = 1 / mb;
+    const float gm1 = c.grid_size - 1.0f;
+    const int nx = (int)rn_clampf(0.5f * fmaf(x, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const int ny = (int)rn_clampf(0.5f * fmaf(y, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const int nz = (int)rn_clampf(0.5f * fmaf(z, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const uint32_t idx = mip * g3 + rn_morton3d(nx, ny, nz);
+    const bool occ = bitfield[idx / 8] & (1 << (idx % 8));
+    if (occ) return true;
+    const float tx = fmaf(fmaf(fmaf(0.5f, rn_signf(dx), nx + 0.5f) * gsi, 2.0f, -1.0f), mb, -x) * dxi;
+    const float ty = fmaf(fmaf(fmaf(0.5f, rn_signf(dy), ny + 0.5f) * gsi, 2.0f, -1.0f), mb, -y) * dyi;
+    const float tz = fmaf(fmaf(fmaf(0.5f, rn_signf(dz), nz + 0.5f) * gsi, 2.0f, -1.0f), mb, -z) * dzi;
+    const float t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    do {
+        t += rn_calc_dt(t, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+    } while (t < t_target);
+    return false;
+}
+
+// Pass 1 (COUNT) or pass 2 (write) of raymarching.cu:200-279 for one ray.
+template <bool COUNT, typename Sink>
+__device__ int march_ray(float ox, float oy, float oz, float dx, float dy, float dz,
+                         float t1, float t2, int n_write, int start,
+                         const uint8_t* __restrict__ bitfield, const MarchCfg& c,
+                         const Sink& sink) {
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t = t1;
+    int n = 0;
+    if (COUNT) {
+        while (0 <= t && t < t2 && n < c.max_samples) {
+            float x, y, z, dt;
+            if (march_step(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c, x, y, z, dt)) {
+                t += dt; n++;
+            }
+        }
+    } else {
+        while (t < t2 && n < n_write) {
+            float x, y, z, dt;
+            if (march_step(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c, x, y, z, dt)) {
+                sink.emit(start + n, x, y, z, t, dt);
+                t += dt; n++;
+            }
+        }
+    }
+    return n;
+}
+
+// intersection.cu:5-22 (_ray_aabb_intersect) for a single box
+__device__ __forceinline__ void aabb(float ox, float oy, float oz, float dx, float dy, float dz,
+                                     const float* __restrict__ c, const float* __restrict__ h,
+                                     float& t1, float& t2) {
+    const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
+    const float ax = (c[0] - h[0] - ox) * ix, bx = (c[0] + h[0] - ox) * ix;
+    const float ay = (c[1] - h[1] - oy) * iy, by = (c[1] + h[1] - oy) * iy;
+    const float az = (c[2] - h[2] - oz) * iz, bz = (c[2] + h[2] - oz) * iz;
+    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fminf(az, bz));
+    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz));
+    if (n > f) { t1 = -1.0f; t2 = -1.0f; } else { t1 = n; t2 = f; }
+}
+
+// ----------------------------------------------------------------------------
+// drop-in path: one sub-NeRF, hits_t given (vren.raymarching_train)
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ float perturbed_t1(float t1, float noise, const MarchCfg& c) {
+    if (t1 >= 0) {  // raymarching.cu:195-198
+        const float dt = rn_calc_dt(t1, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+        t1 = fmaf(dt, noise, t1);
+    }
+    return t1;
+}
+
+__global__ void __launch_bounds__(256)
+k_march_train_count(int n_rays, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                    const float* __restrict__ hits_t, const float* __restrict__ noise,
+                    const uint8_t* __restrict__ bitfield, MarchCfg c, int32_t* __restrict__ counts) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const float t1 = perturbed_t1(hits_t[2 * r], noise[r], c);
+    counts[r] = march_ray<true>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2],
+                                rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2],
+                                t1, hits_t[2 * r + 1], 0, 0, bitfield, c, NoSink{});
+}
+
+__global__ void __launch_bounds__(256)
+k_march_train_write(int n_rays, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+                    const float* __restrict__ hits_t, const float* __restrict__ noise,
+                    const uint8_t* __restrict__ bitfield, MarchCfg c,
+                    const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
+                    int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
+                    float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const int n = counts[r], start = offsets[r];
+    rays_a[3 * r + 0] = r; rays_a[3 * r + 1] = start; rays_a[3 * r + 2] = n;
+    if (n == 0) return;
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    const float t1 = perturbed_t1(hits_t[2 * r], noise[r], c);
+    RefSink sink{xyzs, dirs, ts, deltas, dx, dy, dz};
+    march_ray<false>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2], dx, dy, dz,
+                     t1, hits_t[2 * r + 1], n, start, bitfield, c, sink);
+}
+
+// ----------------------------------------------------------------------------
+// single-block exclusive scan with per-segment alignment.
+//   counts: [n_seg][n_per]  ->  offsets (same shape), seg_base[n_seg],
+//   seg_count[n_seg], meta[0] = aligned end, meta[1] = unaligned total.
+// segment k starts at seg_base[k] = align_up(seg_base[k-1] + seg_count[k-1]).
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ counts,
+                int32_t* __restrict__ offsets, int32_t* __restrict__ seg_base,
+                int32_t* __restrict__ seg_count, int32_t* __restrict__ meta) {
+    __shared__ int wsum[16];
+    __shared__ int carry_s;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nthr = blockDim.x, nw = nthr >> 6;
+    int base = 0, total = 0;
+    for (int k = 0; k < n_seg; ++k) {
+        const int32_t* cin = counts + (size_t)k * n_per;
+        int32_t* cout = offsets + (size_t)k * n_per;
+        int carry = 0;
+        for (int c0 = 0; c0 < n_per; c0 += nthr) {
+            const int i = c0 + tid;
+            const int v = i < n_per ? cin[i] : 0;
+            const int incl = rn_wave_incl_sum_i(v);
+            if (lane == 63) wsum[wid] = incl;
+            __syncthreads();
+            if (wid == 0) {
+                int s = lane < nw ? wsum[lane] : 0;
+                s = rn_wave_incl_sum_i(s);
+                if (lane < nw) wsum[lane] = s;
+            }
+            __syncthreads();
+            const int wpre = wid > 0 ? wsum[wid - 1] : 0;
+            if (i < n_per) cout[i] = base + carry + wpre + incl - v;
+            const int chunk_total = wsum[nw - 1];
+            __syncthreads();
+            carry += chunk_total;
+        }
+        if (tid == 0) { seg_base[k] = base; seg_count[k] = carry; }
+        total += carry;
+        base = ((base + carry + align - 1) / align) * align;
+    }
+    if (tid == 0) { meta[0] = base; meta[1] = total; }
+    (void)carry_s;
+}
+
+// ----------------------------------------------------------------------------
+// fused multi-sub-NeRF march (ml_rendering.py:47-52 + __render_rays_train
+// :174-179): AABB + NEAR clamp + jitter + count for K sub-NeRFs in one launch.
+// thread -> (k, r); bitfields: [K][bitfield_bytes]; noise: [K][B]
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_ml_march_count(int n_rays, int K, const float* __restrict__ rays_o,
+                 const float* __restrict__ rays_d, const float* __restrict__ center,
+                 const float* __restrict__ half_size, float near_distance,
+                 const float* __restrict__ noise, const uint8_t* __restrict__ bitfields,
+                 int64_t bitfield_bytes, MarchCfg c, int32_t* __restrict__ counts) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= n_rays * K) return;
+    const int k = gid / n_rays, r = gid - k * n_rays;
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    float t1, t2;
+    aabb(ox, oy, oz, dx, dy, dz, center, half_size, t1, t2);
+    if (!(t2 > 0)) { t1 = -1.0f; t2 = -1.0f; }              // intersection.cu:48
+    else { t1 = fmaxf(t1, 0.0f); if (t1 < near_distance) t1 = near_distance; }
+    t1 = perturbed_t1(t1, noise[gid], c);
+    counts[gid] = march_ray<true>(ox, oy, oz, dx, dy, dz, t1, t2, 0, 0,
+                                  bitfields + (size_t)k * bitfield_bytes, c, NoSink{});
+}
+
+__global__ void __launch_bounds__(256)
+k_ml_march_write(int n_rays, int K, const float* __restrict__ rays_o,
+                 const float* __restrict__ rays_d, const float* __restrict__ center,
+                 const float* __restrict__ half_size, float near_distance,
+                 const float* __restrict__ noise, const uint8_t* __restrict__ bitfields,
+                 int64_t bitfield_bytes, MarchCfg c, const int32_t* __restrict__ counts,
+                 const int32_t* __restrict__ offsets, float* __restrict__ ts,
+                 float* __restrict__ deltas, int32_t* __restrict__ ray_of) {
+    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= n_rays * K) return;
+    const int n = counts[gid];
+    if (n == 0) return;
+    const int k = gid / n_rays, r = gid - k * n_rays;
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    float t1, t2;
+    aabb(ox, oy, oz, dx, dy, dz, center, half_size, t1, t2);
+    t1 = fmaxf(t1, 0.0f);
+    if (t1 < near_distance) t1 = near_distance;
+    t1 = perturbed_t1(t1, noise[gid], c);
+    CompactSink sink{ts, deltas, ray_of, r};
+    march_ray<false>(ox, oy, oz, dx, dy, dz, t1, t2, n, offsets[gid],
+                     bitfields + (size_t)k * bitfield_bytes, c, sink);
+}
+
+// ----------------------------------------------------------------------------
+// test-time march (raymarching.cu:335-404) incl. the calc_dt(cascades) quirk
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_march_test(int n_alive, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
+             float* __restrict__ hits_t, const int64_t* __restrict__ alive,
+             const uint8_t* __restrict__ bitfield, MarchCfg c, int n_samples,
+             float* __restrict__ xyzs, float* __restrict__ dirs, float* __restrict__ deltas,
+             float* __restrict__ ts, int32_t* __restrict__ n_eff) {
+    const int n = blockIdx.x * blockDim.x + threadIdx.x;
+    if (n >= n_alive) return;
+    const int64_t r = alive[n];
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
+    float t = hits_t[2 * r];
+    const float t2 = hits_t[2 * r + 1];
+    int s = 0;
+    const size_t row = (size_t)n * n_samples;
+    while (t < t2 && s < n_samples) {
+        float x, y, z, dt;
+        if (march_step(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c, x, y, z, dt)) {
+            const size_t o = row + s;
+            xyzs[3 * o] = x; xyzs[3 * o + 1] = y; xyzs[3 * o + 2] = z;
+            dirs[3 * o] = dx; dirs[3 * o + 1] = dy; dirs[3 * o + 2] = dz;
+            ts[o] = t; deltas[o] = dt;
+            t += dt;
+            hits_t[2 * r] = t;
+            s++;
+        }
+    }
+    n_eff[n] = s;
+}
+
+// ----------------------------------------------------------------------------
+// ray/AABB intersection (intersection.cu:25-100), deterministic: hits for a
+// ray are kept in voxel order (first max_hits), then sorted by t_near with
+// the reference's torch::sort semantics (unfilled -1 slots sort first).
+// ----------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_ray_aabb(int n_rays, int n_vox, int max_hits, const float* __restrict__ rays_o,
+           const float* __restrict__ rays_d, const float* __restrict__ centers,
+           const float* __restrict__ halfs, int32_t* __restrict__ hit_cnt,
+           float* __restrict__ hits_t, int64_t* __restrict__ hit_idx) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    float* ht = hits_t + (size_t)r * max_hits * 2;
+    int64_t* hi = hit_idx + (size_t)r * max_hits;
+    for (int m = 0; m < max_hits; ++m) { ht[2 * m] = -1.0f; ht[2 * m + 1] = -1.0f; hi[m] = -1; }
+    int cnt = 0;
+    for (int v = 0; v < n_vox; ++v) {
+        float t1, t2;
+        aabb(ox, oy, oz, dx, dy, dz, centers + 3 * v, halfs + 3 * v, t1, t2);
+        if (t2 > 0) {
+            if (cnt < max_hits) {
+                ht[2 * cnt] = fmaxf(t1, 0.0f); ht[2 * cnt + 1] = t2; hi[cnt] = v;
+            }
+            cnt++;
+        }
+    }
+    hit_cnt[r] = cnt;
+    // stable insertion sort of the max_hits slots by t_near (torch::sort asc)
+    for (int a = 1; a < max_hits; ++a) {
+        const float k0 = ht[2 * a], k1 = ht[2 * a + 1];
+        const int64_t kv = hi[a];
+        int b = a - 1;
+        while (b >= 0 && ht[2 * b] > k0) {
+            ht[2 * (b + 1)] = ht[2 * b]; ht[2 * (b + 1) + 1] = ht[2 * b + 1]; hi[b + 1] = hi[b];
+            --b;
+        }
+        ht[2 * (b + 1)] = k0; ht[2 * (b + 1) + 1] = k1; hi[b + 1] = kv;
+    }
+}
+
+inline MarchCfg make_cfg(int cascades, int grid_size, int max_samples, float scale,
+                         float dt_scale, float esf) {
+    MarchCfg c;
+    c.cascades = cascades; c.grid_size = grid_size; c.max_samples = max_samples;
+    c.scale = scale; c.dt_scale = dt_scale; c.esf = esf;
+    return c;
+}
+
+inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+}  // namespace
+
+// ============================================================================
+// C ABI
+// ============================================================================
+extern "C" {
+
+int rn_ray_aabb_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                          const float* half_sizes, int64_t n_rays, int64_t n_voxels,
+                          int32_t max_hits, int32_t* hit_cnt, float* hits_t,
+                          int64_t* hits_voxel_idx, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_voxels >= 0 && max_hits >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && centers && half_sizes && hit_cnt && hits_t && hits_voxel_idx,
+                 "null pointer");
+    k_ray_aabb<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, (int)n_voxels, max_hits, rays_o, rays_d, centers, half_sizes, hit_cnt,
+        hits_t, hits_voxel_idx);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_raymarching_train_count(const float* rays_o, const float* rays_d, const float* hits_t,
+                               const uint8_t* density_bitfield, int32_t cascades, float scale,
+                               float exp_step_factor, const float* noise, int32_t grid_size,
+                               int32_t max_samples, int64_t n_rays, int32_t* counts,
+                               void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && cascades >= 1 && grid_size >= 1 && grid_size <= 1024 &&
+                 max_samples >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && hits_t && density_bitfield && noise && counts, "null pointer");
+    MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
+    k_march_train_count<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, rays_o, rays_d, hits_t, noise, density_bitfield, c, counts);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_scan_segments(const int32_t* counts, int32_t n_seg, int64_t n_per, int32_t align,
+                     int32_t* offsets, int32_t* seg_base, int32_t* seg_count, int32_t* meta,
+                     void* stream) {
+    RN_CHECK_ARG(n_seg >= 1 && n_per >= 0 && align >= 1, "bad sizes");
+    RN_CHECK_ARG(counts && offsets && seg_base && seg_count && meta, "null pointer");
+    k_scan_segments<<<1, 1024, 0, (hipStream_t)stream>>>(n_seg, (int)n_per, align, counts,
+                                                         offsets, seg_base, seg_count, meta);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_raymarching_train_write(const float* rays_o, const float* rays_d, const float* hits_t,
+                               const uint8_t* density_bitfield, int32_t cascades, float scale,
+                               float exp_step_factor, const float* noise, int32_t grid_size,
+                               int32_t max_samples, int64_t n_rays, const int32_t* counts,
+                               const int32_t* offsets, int64_t* rays_a, float* xyzs, float* dirs,
+                               float* deltas, float* ts, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && cascades >= 1 && grid_size >= 1 && max_samples >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && hits_t && density_bitfield && noise && counts && offsets &&
+                 rays_a, "null pointer");
+    MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
+    k_march_train_write<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, rays_o, rays_d, hits_t, noise, density_bitfield, c, counts, offsets, rays_a,
+        xyzs, dirs, deltas, ts);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_raymarching_test(const float* rays_o, const float* rays_d, float* hits_t,
+                        const int64_t* alive_indices, int64_t n_alive,
+                        const uint8_t* density_bitfield, int32_t cascades, float scale,
+                        float exp_step_factor, int32_t grid_size, int32_t max_samples,
+                        int32_t n_samples, float* xyzs, float* dirs, float* deltas, float* ts,
+                        int32_t* n_eff_samples, void* stream) {
+    RN_CHECK_ARG(n_alive >= 0 && cascades >= 1 && grid_size >= 1 && max_samples >= 1 &&
+                 n_samples >= 1, "bad sizes");
+    if (n_alive == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && hits_t && alive_indices && density_bitfield && xyzs && dirs &&
+                 deltas && ts && n_eff_samples, "null pointer");
+    // raymarching.cu:370,399: calc_dt receives `cascades` as its scale argument
+    MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, (float)cascades,
+                          exp_step_factor);
+    k_march_test<<<nblk(n_alive, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_alive, rays_o, rays_d, hits_t, alive_indices, density_bitfield, c, n_samples, xyzs,
+        dirs, deltas, ts, n_eff_samples);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* center,
+                      const float* half_size, float near_distance, const float* noise,
+                      const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
+                      int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
+                      int32_t max_samples, int64_t n_rays, int32_t* counts, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && cascades >= 1 && grid_size >= 1 &&
+                 max_samples >= 1, "bad sizes");
+    RN_CHECK_ARG(bitfield_bytes >= (int64_t)cascades * grid_size * grid_size * grid_size / 8,
+                 "bitfield too small");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts,
+                 "null pointer");
+    MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
+    k_ml_march_count<<<nblk(n_rays * n_models, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
+        density_bitfields, bitfield_bytes, c, counts);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_ml_march_write(const float* rays_o, const float* rays_d, const float* center,
+                      const float* half_size, float near_distance, const float* noise,
+                      const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
+                      int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
+                      int32_t max_samples, int64_t n_rays, const int32_t* counts,
+                      const int32_t* offsets, float* ts, float* deltas, int32_t* ray_of,
+                      void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && cascades >= 1 && grid_size >= 1 &&
+                 max_samples >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts &&
+                 offsets && ts && deltas && ray_of, "null pointer");
+    MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
+    k_ml_march_write<<<nblk(n_rays * n_models, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
+        density_bitfields, bitfield_bytes, c, counts, offsets, ts, deltas, ray_of);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,133 @@
+// Shared device helpers for the Rad-NeRF MI355X (gfx950) hot path.
+//
+// Floating-point contraction policy (DESIGN.md §"Contraction policy"): every
+// translation unit is compiled under `#pragma clang fp contract(off)`; the
+// multiply-add sites that nvcc fuses in the reference (raymarching.cu:197,205,
+// 215,225,229) are written as explicit fmaf() calls.  The CPU oracle
+// (oracle/vren_oracle.c) uses the identical explicit-fmaf policy, which is what
+// makes per-ray sample counts and sample positions bit-exact between the two.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+#define RN_SQRT3 1.73205080757f
+#define RN_WAVE 64
+
+// ---------------------------------------------------------------------------
+// status / error plumbing shared by every C-ABI entry point
+// ---------------------------------------------------------------------------
+extern "C" void rn_set_error(const char* fmt, ...);
+
+#define RN_CHECK_ARG(cond, msg)                                   \
+    do {                                                          \
+        if (!(cond)) { rn_set_error("%s: %s", __func__, msg);     \
+                       return 1; }                                \
+    } while (0)
+
+#define RN_CHECK_LAUNCH()                                                  \
+    do {                                                                   \
+        hipError_t _e = hipGetLastError();                                 \
+        if (_e != hipSuccess) {                                            \
+            rn_set_error("%s: launch failed: %s", __func__,                \
+                         hipGetErrorString(_e));                           \
+            return 2;                                                      \
+        }                                                                  \
+    } while (0)
+
+// ---------------------------------------------------------------------------
+// reference math helpers (raymarching.cu:7-60, helper_math.h:280-283)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float rn_signf(float x) { return copysignf(1.0f, x); }
+
+// helper_math.h:280  clamp(f,a,b) = fmaxf(a, fminf(f, b))
+__device__ __forceinline__ float rn_clampf(float f, float a, float b) {
+    return fmaxf(a, fminf(f, b));
+}
+
+// raymarching.cu:11-13 (calc_dt).  `scale` is a float parameter; the test-time
+// kernel passes `cascades` there (raymarching.cu:370,399) and so do we.
+__device__ __forceinline__ float rn_calc_dt(float t, float esf, int max_samples,
+                                            int grid_size, float scale) {
+    return rn_clampf(t * esf, RN_SQRT3 / max_samples,
+                     RN_SQRT3 * 2 * scale / grid_size);
+}
+
+// raymarching.cu:19-23
+__device__ __forceinline__ int rn_mip_from_pos(float x, float y, float z, int cascades) {
+    const float mx = fmaxf(fabsf(x), fmaxf(fabsf(y), fabsf(z)));
+    int e;
+    frexpf(mx, &e);
+    return min(cascades - 1, max(0, e + 1));
+}
+
+// raymarching.cu:29-32
+__device__ __forceinline__ int rn_mip_from_dt(float dt, int grid_size, int cascades) {
+    int e;
+    frexpf(dt * grid_size, &e);
+    return min(cascades - 1, max(0, e));
+}
+
+// raymarching.cu:35-60 (Morton coding, 10 bits per axis)
+__host__ __device__ __forceinline__ uint32_t rn_expand_bits(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+__host__ __device__ __forceinline__ uint32_t rn_morton3d(uint32_t x, uint32_t y, uint32_t z) {
+    return rn_expand_bits(x) | (rn_expand_bits(y) << 1) | (rn_expand_bits(z) << 2);
+}
+__host__ __device__ __forceinline__ uint32_t rn_morton3d_invert(uint32_t x) {
+    x = x & 0x49249249u;
+    x = (x | (x >> 2)) & 0xc30c30c3u;
+    x = (x | (x >> 4)) & 0x0f00f00fu;
+    x = (x | (x >> 8)) & 0xff0000ffu;
+    x = (x | (x >> 16)) & 0x0000ffffu;
+    return x;
+}
+
+// ---------------------------------------------------------------------------
+// wave64 collectives
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int rn_lane() { return threadIdx.x & (RN_WAVE - 1); }
+
+__device__ __forceinline__ float rn_wave_sum(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// inclusive prefix sum across the 64 lanes of a wave
+__device__ __forceinline__ float rn_wave_incl_sum(float v) {
+    const int lane = rn_lane();
+#pragma unroll
+    for (int off = 1; off < RN_WAVE; off <<= 1) {
+        float o = __shfl_up(v, off);
+        if (lane >= off) v += o;
+    }
+    return v;
+}
+
+// inclusive prefix product across the 64 lanes of a wave
+__device__ __forceinline__ float rn_wave_incl_prod(float v) {
+    const int lane = rn_lane();
+#pragma unroll
+    for (int off = 1; off < RN_WAVE; off <<= 1) {
+        float o = __shfl_up(v, off);
+        if (lane >= off) v *= o;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int rn_wave_incl_sum_i(int v) {
+    const int lane = rn_lane();
+#pragma unroll
+    for (int off = 1; off < RN_WAVE; off <<= 1) {
+        int o = __shfl_up(v, off);
+        if (lane >= off) v += o;
+    }
+    return v;
+}

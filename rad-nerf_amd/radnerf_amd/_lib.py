@@ -1,0 +1,97 @@
+"""ctypes binding of librn.so (include/radnerf.h).
+
+The library is the product: there is no CPU fallback.  Loading fails loudly
+when librn.so is missing, and every call checks the returned status and raises
+RuntimeError with the library's message (mirroring the TORCH_CHECK errors of
+models/csrc/include/utils.h:4-6 in the reference).  ctypes releases the GIL
+for the duration of each call.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("RADNERF_LIB", os.path.join(_HERE, "librn.so"))
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+I64 = ctypes.c_int64
+F32 = ctypes.c_float
+
+# name -> argtypes (all return int status).  Keep in sync with include/radnerf.h
+SIGNATURES = {
+    "rn_ray_aabb_intersect": [P, P, P, P, I64, I64, I32, P, P, P, P],
+    "rn_raymarching_train_count": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P],
+    "rn_raymarching_train_write": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P, P, P, P,
+                                   P, P, P],
+    "rn_scan_segments": [P, I32, I64, I32, P, P, P, P, P],
+    "rn_raymarching_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
+    "rn_ml_march_count": [P, P, P, P, F32, P, P, I64, I32, I32, F32, F32, I32, I32, I64, P, P],
+    "rn_ml_march_write": [P, P, P, P, F32, P, P, I64, I32, I32, F32, F32, I32, I32, I64, P, P,
+                          P, P, P, P],
+    "rn_composite_train_fw": [P, P, P, P, P, I64, F32, P, P, P, P, P, P],
+    "rn_composite_train_bw": [P, P, P, P, P, P, P, P, P, P, I64, P, P, P, F32, P, P, P],
+    "rn_composite_test_fw": [P, P, P, P, I64, I32, P, F32, P, P, P, P, P],
+    "rn_ml_composite_fw": [P, P, P, P, P, P, I64, I32, F32, P, P, P, P, P, P],
+    "rn_ml_combine_fw": [P, P, P, P, P, I64, I32, P, P, P, P],
+    "rn_ml_combine_bw": [P, P, P, P, P, I64, I32, P, P],
+    "rn_ml_composite_bw": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P],
+    "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, I32, P],
+    "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                     I32, P],
+    "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
+    "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, P, I32, I32, P],
+    "rn_pack_f16": [P, I64, P, I64, I32, I64, P, P],
+    "rn_to_f16": [P, I64, P, P],
+    "rn_morton3d": [P, I64, P, P],
+    "rn_morton3d_invert": [P, I64, P, P],
+    "rn_packbits": [P, I64, F32, P, P],
+}
+
+_lib = None
+
+
+class _Checked:
+    def __init__(self, lib, name):
+        self._fn = getattr(lib, name)
+        self._fn.argtypes = SIGNATURES[name]
+        self._fn.restype = ctypes.c_int
+        self._name = name
+        self._err = lib.rn_last_error
+
+    def __call__(self, *args):
+        st = self._fn(*args)
+        if st != 0:
+            msg = self._err().decode("utf-8", "replace")
+            raise RuntimeError(f"{self._name} failed (status {st}): {msg}")
+        return st
+
+
+class _Lib:
+    def __init__(self, path):
+        if not os.path.exists(path):
+            raise ImportError(
+                f"radnerf_amd: HIP library not found at {path}; build it with "
+                f"`make -C rad-nerf_amd/csrc` (hipcc --offload-arch=gfx950). There is no CPU "
+                f"fallback.")
+        self.handle = ctypes.CDLL(path)
+        self.handle.rn_last_error.restype = ctypes.c_char_p
+        self.handle.rn_last_error.argtypes = []
+        self.handle.rn_version.restype = ctypes.c_int
+        self.path = path
+        for name in SIGNATURES:
+            setattr(self, name[3:], _Checked(self.handle, name))
+
+    def version(self):
+        return self.handle.rn_version()
+
+
+def lib():
+    """The loaded librn.so (raises ImportError when it is missing)."""
+    global _lib
+    if _lib is None:
+        _lib = _Lib(LIB_PATH)
+    return _lib
+
+
+def exported_symbols():
+    return ["rn_version", "rn_last_error"] + list(SIGNATURES)

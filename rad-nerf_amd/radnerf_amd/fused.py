@@ -1,0 +1,234 @@
+"""Fused Rad-NeRF training render: the whole hot path of ml_render
+(models/ml_rendering.py:11-78 + :158-202) for all K sub-NeRFs as a fixed
+chain of HIP launches with no host synchronisation:
+
+  forward : gate_fwd -> ml_march_count -> scan_segments -> ml_march_write
+            -> field_fwd (all K models, compact samples) -> ml_composite_fw
+            -> ml_combine_fw
+  backward: ml_combine_bw -> ml_composite_bw -> field_bwd -> gate_bwd
+
+Sample buffers are sized for the worst case (B*K*max_samples, + alignment),
+so sample counts never have to be read back; every kernel consumes the
+device-side counts.  Outputs equal the unfused drop-in path (rendering.py)
+for the same noise (tests/test_gpu_parity.py).
+"""
+import torch
+
+from . import layout as LY
+from ._lib import lib
+
+MAX_SAMPLES = 1024
+NEAR_DISTANCE = 0.01
+SEG_ALIGN = 128
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+class Workspace:
+    """Persistent device buffers for one (B, K) configuration."""
+
+    def __init__(self, n_rays, n_models, device, max_samples=MAX_SAMPLES, capacity=None):
+        B, K = n_rays, n_models
+        self.B, self.K, self.device = B, K, device
+        cap = capacity or (B * K * max_samples + SEG_ALIGN * K)
+        self.capacity = cap
+        f = dict(device=device, dtype=torch.float32)
+        i = dict(device=device, dtype=torch.int32)
+        self.counts = torch.empty(K, B, **i)
+        self.offsets = torch.empty(K, B, **i)
+        self.seg = torch.zeros(2 * K + 2, **i)      # seg_base[K] | seg_count[K] | meta[2]
+        self.used = torch.empty(K, B, **i)
+        self.ts = torch.empty(cap, **f)
+        self.deltas = torch.empty(cap, **f)
+        self.ray_of = torch.empty(cap, **i)
+        self.sigma = torch.empty(cap, **f)
+        self.rgb = torch.empty(cap, 3, **f)
+        self.ws = torch.empty(cap, **f)
+        self.dsigma = torch.empty(cap, **f)
+        self.drgb = torch.empty(cap, 3, **f)
+        self.opacity_k = torch.empty(K, B, **f)
+        self.depth_k = torch.empty(K, B, **f)
+        self.rgb_k = torch.empty(K, B, 3, **f)
+        self.dgate = torch.empty(B, K, **f)
+
+    @property
+    def seg_base(self):
+        return self.seg[: self.K]
+
+    @property
+    def seg_count(self):
+        return self.seg[self.K: 2 * self.K]
+
+    @property
+    def meta(self):
+        return self.seg[2 * self.K:]
+
+    def n_samples(self):
+        """Total marched samples (reads back: diagnostics only)."""
+        return int(self.meta[1].item())
+
+
+class FusedMLRenderer:
+    """Owns the workspace and runs the fused forward / backward chains."""
+
+    def __init__(self, model, gating_net, n_rays, device=None, fwd_blocks=None, bwd_blocks=None,
+                 capacity=None):
+        self.model, self.gate = model, gating_net
+        self.device = device or model.mlp_params.device
+        self.ws = Workspace(n_rays, model.size, self.device, capacity=capacity)
+        K = model.size
+        bf = [getattr(model, f"density_bitfield_{i}") for i in range(K)]
+        self.bitfield_bytes = bf[0].numel()
+        self.fwd_blocks = fwd_blocks or max(1, 2048 // K)
+        self.bwd_blocks = bwd_blocks or max(1, 256 // K)
+
+    def bitfields(self):
+        K = self.model.size
+        bf = [getattr(self.model, f"density_bitfield_{i}") for i in range(K)]
+        if all(b.data_ptr() == bf[0].data_ptr() + i * self.bitfield_bytes for i, b in enumerate(bf)):
+            return bf[0]
+        self._bf = torch.stack(bf).contiguous()
+        return self._bf
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, rays_o, rays_d, gate_in2, noise, bg, T_threshold=1e-4,
+                exp_step_factor=0.0):
+        m, g, w, L = self.model, self.gate, self.ws, lib()
+        B, K = rays_o.shape[0], m.size
+        assert B == w.B and noise.shape == (K, B)
+        st = _stream(rays_o.device)
+        out_gate = torch.empty(B, K, device=rays_o.device)
+        imp = torch.zeros(K, device=rays_o.device)
+        L.gate_fwd(rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K, g.packed_frags().data_ptr(),
+                   out_gate.data_ptr(), imp.data_ptr(), max(1, min(256, (B + 127) // 128)), st)
+        bits = self.bitfields()
+        march = (rays_o.data_ptr(), rays_d.data_ptr(), m.center.data_ptr(),
+                 m.half_size.data_ptr(), NEAR_DISTANCE, noise.data_ptr(), bits.data_ptr(),
+                 self.bitfield_bytes, K, m.cascades, float(m.scale), float(exp_step_factor),
+                 m.grid_size, MAX_SAMPLES, B)
+        L.ml_march_count(*march, w.counts.data_ptr(), st)
+        L.scan_segments(w.counts.data_ptr(), K, B, SEG_ALIGN, w.offsets.data_ptr(),
+                        w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.meta.data_ptr(), st)
+        L.ml_march_write(*march, w.counts.data_ptr(), w.offsets.data_ptr(), w.ts.data_ptr(),
+                         w.deltas.data_ptr(), w.ray_of.data_ptr(), st)
+        self._field(True, rays_o, rays_d, st)
+        L.ml_composite_fw(w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
+                          w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
+                          float(T_threshold), w.used.data_ptr(), w.opacity_k.data_ptr(),
+                          w.depth_k.data_ptr(), w.rgb_k.data_ptr(), w.ws.data_ptr(), st)
+        rgb = torch.empty(B, 3, device=rays_o.device)
+        opacity = torch.empty(B, device=rays_o.device)
+        depth = torch.empty(B, K, device=rays_o.device)
+        L.ml_combine_fw(out_gate.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
+                        w.rgb_k.data_ptr(), bg.data_ptr(), B, K, rgb.data_ptr(),
+                        opacity.data_ptr(), depth.data_ptr(), st)
+        return rgb, opacity, depth, out_gate, imp
+
+    def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
+        m, w, L = self.model, self.ws, lib()
+        lo, lh, lr, ls = m.xyz_encoder.level_ptrs()
+        common = (None, None, 0, w.ts.data_ptr(), w.ray_of.data_ptr(), rays_o.data_ptr(),
+                  rays_d.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(), m.size,
+                  m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
+                  m._h_ext.ctypes.data, m.packed_frags().data_ptr())
+        if fwd:
+            L.field_fwd(*common, w.sigma.data_ptr(), w.rgb.data_ptr(), self.fwd_blocks, st)
+        else:
+            L.field_bwd(*common, m.dw_map(rays_o.device).data_ptr(), w.dsigma.data_ptr(),
+                        w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(), self.bwd_blocks,
+                        st)
+
+    # ----------------------------------------------------------------- backward
+    def backward(self, rays_o, rays_d, gate_in2, gate, bg, dL_drgb, dL_dopacity, dL_ddepth,
+                 dL_dgate_ext=None, T_threshold=1e-4, grid_grad=None, mlp_grad=None,
+                 gate_grad=None):
+        """Accumulates into grid_grad / mlp_grad / gate_grad (zero-initialised
+        by the caller or allocated here) and returns them."""
+        m, g, w, L = self.model, self.gate, self.ws, lib()
+        B, K = rays_o.shape[0], m.size
+        dev = rays_o.device
+        st = _stream(dev)
+        grid_grad = torch.zeros_like(m.xyz_encoder.params) if grid_grad is None else grid_grad
+        mlp_grad = torch.zeros_like(m.mlp_params) if mlp_grad is None else mlp_grad
+        gate_grad = torch.zeros_like(g.params) if gate_grad is None else gate_grad
+        L.ml_combine_bw(dL_drgb.data_ptr(), dL_dopacity.data_ptr(), w.opacity_k.data_ptr(),
+                        w.rgb_k.data_ptr(), bg.data_ptr(), B, K, w.dgate.data_ptr(), st)
+        if dL_dgate_ext is not None:
+            w.dgate.add_(dL_dgate_ext)
+        L.ml_composite_bw(dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
+                          None if dL_ddepth is None else dL_ddepth.data_ptr(), gate.data_ptr(),
+                          bg.data_ptr(), w.sigma.data_ptr(), w.rgb.data_ptr(),
+                          w.deltas.data_ptr(), w.ts.data_ptr(), w.counts.data_ptr(),
+                          w.offsets.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
+                          w.rgb_k.data_ptr(), B, K, float(T_threshold), w.dsigma.data_ptr(),
+                          w.drgb.data_ptr(), st)
+        self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
+        L.gate_bwd(rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K, g.packed_frags().data_ptr(),
+                   g.dw_map(dev).data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
+                   gate_grad.numel(), max(1, min(128, (B + 127) // 128)), st)
+        return grid_grad, mlp_grad, gate_grad
+
+
+class _MLRenderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, grid_params, mlp_params, gate_params, renderer, rays_o, rays_d, gate_in2,
+                noise, bg, T_threshold, esf):
+        rgb, opacity, depth, gate, imp = renderer.forward(rays_o, rays_d, gate_in2, noise, bg,
+                                                          T_threshold, esf)
+        ctx.renderer = renderer
+        ctx.save_for_backward(rays_o, rays_d, gate_in2, gate, bg)
+        ctx.T = T_threshold
+        return rgb, opacity, depth, gate
+
+    @staticmethod
+    def backward(ctx, d_rgb, d_op, d_depth, d_gate):
+        rays_o, rays_d, gate_in2, gate, bg = ctx.saved_tensors
+        B, K = gate.shape
+        dev = rays_o.device
+        z = lambda *s: torch.zeros(*s, device=dev)
+        d_rgb = z(B, 3) if d_rgb is None else d_rgb.float().contiguous()
+        d_op = z(B) if d_op is None else d_op.float().contiguous()
+        d_depth = None if d_depth is None else d_depth.float().contiguous()
+        d_gate = None if d_gate is None else d_gate.float().contiguous()
+        gg, mg, ag = ctx.renderer.backward(rays_o, rays_d, gate_in2, gate, bg, d_rgb, d_op,
+                                           d_depth, d_gate, ctx.T)
+        return gg, mg, ag, None, None, None, None, None, None, None, None
+
+
+_RENDERERS = {}
+
+
+def get_renderer(model, gating_net, n_rays):
+    key = (id(model), id(gating_net), n_rays, str(model.mlp_params.device))
+    r = _RENDERERS.get(key)
+    if r is None:
+        r = FusedMLRenderer(model, gating_net, n_rays)
+        _RENDERERS[key] = r
+    return r
+
+
+def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):
+    """Same result dict as ml_rendering.ml_render (train mode)."""
+    rays_o, rays_d = rays_o.float().contiguous(), rays_d.float().contiguous()
+    second = imgs_d.float().contiguous() if gating_net.type == "image" else rays_d
+    B, K, dev = rays_o.shape[0], model.size, rays_o.device
+    esf = float(kwargs.get("exp_step_factor", 0.0))
+    noise = kwargs.get("noise")
+    if noise is None:
+        noise = torch.rand(K, B, device=dev)
+    if esf == 0:
+        bg = torch.ones(3, device=dev)
+    elif kwargs.get("random_bg", False):
+        bg = torch.rand(3, device=dev)
+    else:
+        bg = torch.zeros(3, device=dev)
+    r = get_renderer(model, gating_net, B)
+    rgb, opacity, depth, gate = _MLRenderFn.apply(
+        model.xyz_encoder.params, model.mlp_params, gating_net.params, r, rays_o, rays_d, second,
+        noise.contiguous(), bg, float(kwargs.get("T_threshold", 1e-4)), esf)
+    w = r.ws
+    singles = [(w.rgb_k[i] + bg * (1 - w.opacity_k[i])[:, None]).detach() for i in range(K)]
+    return {"rgb": rgb, "independent_rgbs": singles, "depth": depth, "opacity": opacity,
+            "gating_code": gate, "gating_importance": gate.sum(0)}

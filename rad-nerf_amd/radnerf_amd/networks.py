@@ -1,0 +1,380 @@
+"""Field and gate modules of Rad-NeRF on the HIP kernels.
+
+Mirrors the reference modules' interface (models/networks.py):
+  * MNGP(scale, rgb_act='Sigmoid', size=2, t=19)     networks.py:214-421
+      forward(x, d, ind) -> (sigmas (N) f32, rgbs (N,3) f32)
+      density(x, ind, return_feat=False) -> sigmas
+      update_density_grid(...) / sample_uniform_and_occupied_cells / get_all_cells
+      buffers center, xyz_min, xyz_max, half_size, grid_coords,
+              density_bitfield_{i}, density_grid_{i}; attrs scale, cascades, grid_size, size
+  * NGP(scale, rgb_act='Sigmoid', t=19)               networks.py:17-211 (single model)
+  * Ray_Gate(out_dim, type='ray')                     networks.py:1070-1097
+      forward(x (B,6), warmup=False) -> (gate (B,K), importance (K), None)
+
+Parameters are fp32 masters: `xyz_encoder.params` (hash table, (entries*2,)),
+`mlp_params` (size, 9472) and `Ray_Gate.params`.  The kernels read f16 copies
+(hash table) and f16 MFMA fragments (MLPs) packed from the masters by HIP
+kernels whenever the master changed (tracked with the tensor version counter).
+tcnn's own flat-parameter ordering is not reproduced (unpinned dependency).
+"""
+import math
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import layout as LY
+from . import vren
+from ._lib import lib
+
+RGB_ACTS = ("Sigmoid",)
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _xavier_(mat, gen):
+    fan_out, fan_in = mat.shape
+    bound = math.sqrt(6.0 / (fan_in + fan_out))
+    with torch.no_grad():
+        mat.uniform_(-bound, bound, generator=gen)
+
+
+class _DeviceTables:
+    """Per-device cache of the int index tables (layout.py)."""
+    _cache = {}
+
+    @classmethod
+    def get(cls, key, device, builder):
+        k = (key, str(device))
+        if k not in cls._cache:
+            cls._cache[k] = torch.from_numpy(builder()).to(device)
+        return cls._cache[k]
+
+
+class HashGridEncoding(nn.Module):
+    """tcnn Grid/Hash encoding parameters (networks.py:234-247): L=16, F=2,
+    T=2^t, N_min=16, per_level_scale = exp(log(2048*scale/16)/15)."""
+
+    def __init__(self, scale, log2_T=19, generator=None):
+        super().__init__()
+        self.levels = LY.grid_levels(scale, log2_T)
+        self.n_entries = int(self.levels["n_entries"])
+        self.n_levels, self.n_output_dims = LY.N_LEVELS, LY.N_LEVELS * LY.N_FEATURES
+        p = torch.empty(self.n_entries * 2)
+        p.uniform_(-1e-4, 1e-4, generator=generator)
+        self.params = nn.Parameter(p)
+        self._f16 = None
+        self._f16_ver = None
+        # host copies handed to the kernels
+        self.h_offset = np.ascontiguousarray(self.levels["offset"], np.uint32)
+        self.h_hsize = np.ascontiguousarray(self.levels["hsize"], np.uint32)
+        self.h_res = np.ascontiguousarray(self.levels["res"], np.uint32)
+        self.h_scale = np.ascontiguousarray(self.levels["scale"], np.float32)
+
+    def level_ptrs(self):
+        return (self.h_offset.ctypes.data, self.h_hsize.ctypes.data, self.h_res.ctypes.data,
+                self.h_scale.ctypes.data)
+
+    def params_f16(self):
+        """f16 copy of the table (tcnn keeps the table in f16), refreshed when
+        the fp32 master changes."""
+        p = self.params
+        if self._f16 is None or self._f16.device != p.device or self._f16_ver != p._version:
+            if self._f16 is None or self._f16.device != p.device:
+                self._f16 = torch.empty(p.numel(), dtype=torch.float16, device=p.device)
+            lib().to_f16(p.data_ptr(), p.numel(), self._f16.data_ptr(), _stream(p.device))
+            self._f16_ver = p._version
+        return self._f16
+
+
+class _FieldFn(torch.autograd.Function):
+    """MNGP.forward(x, d, ind) on rn_field_fwd / rn_field_bwd."""
+
+    @staticmethod
+    def forward(ctx, xyzs, dirs, grid_params, mlp_params, model, ind):
+        xyzs = xyzs.float().contiguous()
+        dirs = dirs.float().contiguous()
+        n = xyzs.shape[0]
+        dev = xyzs.device
+        sigma = torch.empty(n, device=dev)
+        rgb = torch.empty(n, 3, device=dev)
+        if n > 0:
+            model._launch_field(True, xyzs, dirs, ind, sigma=sigma, rgb=rgb)
+        ctx.save_for_backward(xyzs, dirs)
+        ctx.model, ctx.ind = model, ind
+        return sigma, rgb
+
+    @staticmethod
+    def backward(ctx, dsigma, drgb):
+        xyzs, dirs = ctx.saved_tensors
+        model, ind = ctx.model, ctx.ind
+        dev = xyzs.device
+        grid_grad = torch.zeros_like(model.xyz_encoder.params)
+        dw = torch.zeros_like(model.mlp_params)
+        if xyzs.shape[0] > 0:
+            ds = torch.zeros(xyzs.shape[0], device=dev) if dsigma is None else dsigma.float().contiguous()
+            dr = torch.zeros(xyzs.shape[0], 3, device=dev) if drgb is None else drgb.float().contiguous()
+            model._launch_field(False, xyzs, dirs, ind, dsigma=ds, drgb=dr, grid_grad=grid_grad,
+                                dw=dw)
+        return None, None, grid_grad, dw, None, None
+
+
+class MNGP(nn.Module):
+    """networks.py:214-421 on the HIP field kernels."""
+
+    def __init__(self, scale, rgb_act="Sigmoid", size=2, t=19, seed=None):
+        super().__init__()
+        if rgb_act not in RGB_ACTS:
+            raise ValueError(f"rgb_act {rgb_act} not supported (only {RGB_ACTS})")
+        self.rgb_act = rgb_act
+        self.scale = scale
+        self.register_buffer("center", torch.zeros(1, 3))
+        self.register_buffer("xyz_min", -torch.ones(1, 3) * scale)
+        self.register_buffer("xyz_max", torch.ones(1, 3) * scale)
+        self.register_buffer("half_size", (self.xyz_max - self.xyz_min) / 2)
+        self.size = size
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        self.xyz_encoder = HashGridEncoding(scale, t, gen)
+        self.cascades = LY.cascades_for_scale(scale)
+        self.grid_size = 128
+        g = torch.arange(self.grid_size, dtype=torch.int32)
+        coords = torch.stack(torch.meshgrid(g, g, g, indexing="ij"), -1).reshape(-1, 3)
+        # kornia create_meshgrid3d(..., False) order: (x fastest) -> coords[:, (2,1,0)]
+        self.register_buffer("grid_coords", coords[:, [2, 1, 0]].contiguous())
+        for i in range(size):
+            self.register_buffer(f"density_bitfield_{i}",
+                                 torch.zeros(self.cascades * self.grid_size ** 3 // 8,
+                                             dtype=torch.uint8))
+            self.register_buffer(f"density_grid_{i}",
+                                 torch.zeros(self.cascades, self.grid_size ** 3))
+        mlp = torch.empty(size, LY.FIELD_PARAMS)
+        for i in range(size):
+            for name, mat in LY.split_field_params(mlp[i]).items():
+                _xavier_(mat, gen)
+        self.mlp_params = nn.Parameter(mlp)
+        self._frags = None
+        self._frags_ver = None
+        self._set_box_host()
+
+    # ---------------------------------------------------------------- plumbing
+    def _set_box_host(self):
+        mn = self.xyz_min.detach().float().cpu().numpy().reshape(3)
+        mx = self.xyz_max.detach().float().cpu().numpy().reshape(3)
+        self._h_min = np.ascontiguousarray(mn, np.float32)
+        self._h_ext = np.ascontiguousarray((mx - mn).astype(np.float32))
+
+    def packed_frags(self):
+        """f16 MFMA fragments of all sub-NeRFs, (size, 46*512) halfs."""
+        p = self.mlp_params
+        if self._frags is None or self._frags.device != p.device or self._frags_ver != p._version:
+            idx = _DeviceTables.get("field_frags", p.device, LY.field_frag_index)
+            if self._frags is None or self._frags.device != p.device:
+                self._frags = torch.empty(self.size, idx.numel(), dtype=torch.float16,
+                                          device=p.device)
+            lib().pack_f16(p.data_ptr(), LY.FIELD_PARAMS, idx.data_ptr(), idx.numel(), self.size,
+                           idx.numel(), self._frags.data_ptr(), _stream(p.device))
+            self._frags_ver = p._version
+        return self._frags
+
+    def dw_map(self, device):
+        return _DeviceTables.get("field_dw", device, LY.field_dw_map)
+
+    def _launch_field(self, fwd, xyzs, dirs, ind, sigma=None, rgb=None, dsigma=None, drgb=None,
+                      grid_grad=None, dw=None, blocks=None):
+        dev = xyzs.device
+        frags = self.packed_frags()
+        grid16 = self.xyz_encoder.params_f16()
+        fptr = frags.data_ptr() + ind * frags.shape[1] * 2
+        lo, lh, lr, ls = self.xyz_encoder.level_ptrs()
+        n = xyzs.shape[0]
+        if fwd:
+            nb = blocks or max(1, min(2048, (n + 127) // 128))
+            lib().field_fwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
+                            None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
+                            self._h_ext.ctypes.data, fptr, sigma.data_ptr(), rgb.data_ptr(), nb,
+                            _stream(dev))
+        else:
+            nb = blocks or max(1, min(512, (n + 255) // 256))
+            lib().field_bwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
+                            None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
+                            self._h_ext.ctypes.data, fptr, self.dw_map(dev).data_ptr(),
+                            dsigma.data_ptr(), drgb.data_ptr(), grid_grad.data_ptr(),
+                            dw.data_ptr() + ind * LY.FIELD_PARAMS * 4, nb, _stream(dev))
+
+    # ------------------------------------------------------------ reference API
+    def density(self, x, ind, return_feat=False):
+        """networks.py:291-309"""
+        if return_feat:
+            raise NotImplementedError("return_feat: use forward(x, d, ind)")
+        d = torch.ones_like(x)
+        sigma, _ = _FieldFn.apply(x, d, self.xyz_encoder.params, self.mlp_params, self, ind)
+        return sigma
+
+    def forward(self, x, d, ind, **kwargs):
+        """networks.py:311-328 -> sigmas (N), rgbs (N,3)"""
+        return _FieldFn.apply(x, d, self.xyz_encoder.params, self.mlp_params, self, ind)
+
+    @torch.no_grad()
+    def get_all_cells(self):
+        """networks.py:330-343"""
+        indices = vren.morton3D(self.grid_coords).long()
+        return [(indices, self.grid_coords)] * self.cascades
+
+    @torch.no_grad()
+    def sample_uniform_and_occupied_cells(self, M, density_threshold, ind):
+        """networks.py:345-372"""
+        cells = []
+        density_grid = getattr(self, f"density_grid_{ind}")
+        for c in range(self.cascades):
+            coords1 = torch.randint(self.grid_size, (M, 3), dtype=torch.int32,
+                                    device=density_grid.device)
+            indices1 = vren.morton3D(coords1).long()
+            indices2 = torch.nonzero(density_grid[c] > density_threshold)[:, 0]
+            if len(indices2) > 0:
+                rand_idx = torch.randint(len(indices2), (M,), device=density_grid.device)
+                indices2 = indices2[rand_idx]
+                coords2 = vren.morton3D_invert(indices2.int())
+                cells += [(torch.cat([indices1, indices2]), torch.cat([coords1, coords2]))]
+            else:
+                cells += [(indices1, coords1)]
+        return cells
+
+    @torch.no_grad()
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
+        """networks.py:375-409"""
+        for i in range(self.size):
+            density_grid = getattr(self, f"density_grid_{i}")
+            density_bitfield = getattr(self, f"density_bitfield_{i}")
+            tmp = torch.zeros_like(density_grid)
+            if warmup:
+                cells = self.get_all_cells()
+            else:
+                cells = self.sample_uniform_and_occupied_cells(self.grid_size ** 3 // 4,
+                                                               density_threshold, i)
+            for c in range(self.cascades):
+                indices, coords = cells[c]
+                s = min(2 ** (c - 1), self.scale)
+                half_grid_size = s / self.grid_size
+                xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
+                xyzs_w += (torch.rand_like(xyzs_w) * 2 - 1) * half_grid_size
+                tmp[c, indices] = self.density(xyzs_w, i)
+            density_grid = torch.where(density_grid < 0, density_grid,
+                                       torch.maximum(density_grid * decay, tmp))
+            mean_density = density_grid[density_grid > 0].mean().item()
+            vren.packbits(density_grid.contiguous(), min(mean_density, density_threshold),
+                          density_bitfield)
+            setattr(self, f"density_grid_{i}", density_grid)
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._set_box_host()
+        return out
+
+
+class NGP(MNGP):
+    """networks.py:17-211: single model; forward(x, d) and buffer
+    `density_bitfield`.  (The reference's CUTLASSMLP and FullyFusedMLP share
+    the no-bias ReLU f16 MLP semantics restated here.)"""
+
+    def __init__(self, scale, rgb_act="Sigmoid", t=19, seed=None):
+        super().__init__(scale, rgb_act, size=1, t=t, seed=seed)
+
+    @property
+    def density_bitfield(self):
+        return self.density_bitfield_0
+
+    @property
+    def density_grid(self):
+        return self.density_grid_0
+
+    def density(self, x, return_feat=False, ind=0):
+        return super().density(x, 0, return_feat)
+
+    def forward(self, x, d, *args, **kwargs):
+        return super().forward(x, d, 0)
+
+    @torch.no_grad()
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
+        super().update_density_grid(density_threshold, warmup, decay, erode)
+
+
+class _GateFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, params, gate_mod):
+        x = x.float().contiguous()
+        B = x.shape[0]
+        K = gate_mod.out_dim
+        dev = x.device
+        gate = torch.empty(B, K, device=dev)
+        imp = torch.zeros(K, device=dev)
+        if B > 0:
+            frags = gate_mod.packed_frags()
+            nb = max(1, min(256, (B + 127) // 128))
+            lib().gate_fwd(x.data_ptr(), x.data_ptr() + 12, 6, B, K, frags.data_ptr(),
+                           gate.data_ptr(), imp.data_ptr(), nb, _stream(dev))
+        ctx.save_for_backward(x)
+        ctx.gate_mod = gate_mod
+        ctx.mark_non_differentiable(imp)
+        return gate, imp
+
+    @staticmethod
+    def backward(ctx, dgate, dimp):
+        (x,) = ctx.saved_tensors
+        g = ctx.gate_mod
+        dw = torch.zeros_like(g.params)
+        B = x.shape[0]
+        if B > 0 and dgate is not None:
+            frags = g.packed_frags()
+            nb = max(1, min(128, (B + 127) // 128))
+            lib().gate_bwd(x.data_ptr(), x.data_ptr() + 12, 6, B, g.out_dim, frags.data_ptr(),
+                           g.dw_map(x.device).data_ptr(), dgate.float().contiguous().data_ptr(),
+                           dw.data_ptr(), dw.numel(), nb, _stream(x.device))
+        return None, dw, None
+
+
+class Ray_Gate(nn.Module):
+    """networks.py:1070-1097: FullyFusedMLP 6 -> 64x4 -> K (ReLU, no bias) +
+    softmax(dim=1); importance = gate.sum(0); top_k_indices = None.
+    Note: like the reference, gradients do not flow into the input x."""
+
+    def __init__(self, out_dim, type="ray", seed=None):
+        super().__init__()
+        if not 1 <= out_dim <= 16:
+            raise ValueError("Ray_Gate supports 1..16 sub-NeRFs")
+        self.out_dim = out_dim
+        self.type = type
+        gen = torch.Generator().manual_seed(seed) if seed is not None else None
+        p = torch.empty(LY.gate_params(out_dim))
+        for _, mat in LY.split_gate_params(p, out_dim).items():
+            _xavier_(mat, gen)
+        self.params = nn.Parameter(p)
+        self._frags = None
+        self._frags_ver = None
+
+    def packed_frags(self):
+        p = self.params
+        if self._frags is None or self._frags.device != p.device or self._frags_ver != p._version:
+            idx = _DeviceTables.get(f"gate_frags_{self.out_dim}", p.device,
+                                    lambda: LY.gate_frag_index(self.out_dim))
+            if self._frags is None or self._frags.device != p.device:
+                self._frags = torch.empty(idx.numel(), dtype=torch.float16, device=p.device)
+            lib().pack_f16(p.data_ptr(), p.numel(), idx.data_ptr(), idx.numel(), 1, idx.numel(),
+                           self._frags.data_ptr(), _stream(p.device))
+            self._frags_ver = p._version
+        return self._frags
+
+    def dw_map(self, device):
+        return _DeviceTables.get(f"gate_dw_{self.out_dim}", device,
+                                 lambda: LY.gate_dw_map(self.out_dim))
+
+    def forward(self, x, warmup=False):
+        gate, _ = _GateFn.apply(x, self.params, self)
+        # importance feeds only the CV^2 loss (losses.py:67-69); keep it on the
+        # autograd graph like the reference's gate.sum(0)
+        return gate, gate.sum(0), None
+
+    def freeze_dict(self):
+        for _, p in self.named_parameters():
+            p.requires_grad_(False)

@@ -1,0 +1,149 @@
+"""Renderer glue (drop-in for models/rendering.py and models/ml_rendering.py).
+
+`render(model, rays_o, rays_d, **kw)`            rendering.py:12-46 (single NGP)
+`ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kw)`
+                                                  ml_rendering.py:11-78 (Rad-NeRF)
+Both keep the reference's autograd structure (RayAABBIntersector ->
+RayMarcher -> model(x, d[, i]) -> VolumeRenderer, then background and the
+gate-weighted combine) and the reference's result keys.  For training with
+model_zoo_size > 1 the fused single-pass path (radnerf_amd.fused) computes the
+same outputs with fewer launches and no host synchronisation; pass
+`fused=True` to route ml_render there.
+
+Test-time rendering follows the host-driven compaction loop of
+ml_rendering.py:81-155 / rendering.py:113-189.
+"""
+import torch
+
+from . import vren
+from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
+
+MAX_SAMPLES = 1024
+NEAR_DISTANCE = 0.01
+
+
+def _near_far(model, rays_o, rays_d):
+    """AABB hits with the NEAR_DISTANCE clamp (ml_rendering.py:48-50)."""
+    _, hits_t, _ = RayAABBIntersector.apply(rays_o, rays_d, model.center, model.half_size, 1)
+    near = hits_t[:, 0, 0]
+    clamp = (near >= 0) & (near < NEAR_DISTANCE)
+    hits_t[clamp, 0, 0] = NEAR_DISTANCE
+    return hits_t
+
+
+def _background(exp_step_factor, random_bg, device):
+    """rendering.py:226-233 / ml_rendering.py:192-198"""
+    if exp_step_factor == 0:
+        return torch.ones(3, device=device)
+    if random_bg:
+        return torch.rand(3, device=device)
+    return torch.zeros(3, device=device)
+
+
+def _train_rays(model, rays_o, rays_d, hits_t, bitfield, call_model, kw):
+    """One model's training render (ml_rendering.py:158-202)."""
+    esf = kw.get("exp_step_factor", 0.0)
+    out = {}
+    rays_a, xyzs, dirs, deltas, ts, n_march = RayMarcher.apply(
+        rays_o, rays_d, hits_t[:, 0], bitfield, model.cascades, model.scale, esf,
+        model.grid_size, MAX_SAMPLES, kw.get("noise"))
+    out["deltas"], out["ts"], out["rm_samples"] = deltas, ts, n_march
+    sigmas, rgbs = call_model(xyzs, dirs)
+    vr, opacity, depth, rgb, ws = VolumeRenderer.apply(
+        sigmas, rgbs.contiguous(), deltas, ts, rays_a, kw.get("T_threshold", 1e-4))
+    bg = _background(esf, kw.get("random_bg", False), rays_o.device)
+    out.update({"vr_samples": vr, "opacity": opacity, "depth": depth, "ws": ws,
+                "rays_a": rays_a, "rgb": rgb + bg * (1 - opacity)[:, None]})
+    return out
+
+
+@torch.no_grad()
+def _test_rays(model, rays_o, rays_d, hits_t, bitfield, call_model, kw):
+    """Progressive-compaction inference (ml_rendering.py:81-155)."""
+    esf = kw.get("exp_step_factor", 0.0)
+    n_rays, dev = rays_o.shape[0], rays_o.device
+    opacity = torch.zeros(n_rays, device=dev)
+    depth = torch.zeros(n_rays, device=dev)
+    rgb = torch.zeros(n_rays, 3, device=dev)
+    alive = torch.arange(n_rays, device=dev)
+    min_samples = 1 if esf == 0 else 4
+    taken, total = 0, 0
+    deltas = None
+    hits0 = hits_t[:, 0].contiguous()
+    while taken < kw.get("max_samples", MAX_SAMPLES):
+        n_alive = alive.shape[0]
+        if n_alive == 0:
+            break
+        step = max(min(n_rays // n_alive, 64), min_samples)
+        taken += step
+        xyzs, dirs, deltas, ts, n_eff = vren.raymarching_test(
+            rays_o, rays_d, hits0, alive, bitfield, model.cascades, model.scale, esf,
+            model.grid_size, MAX_SAMPLES, step)
+        total += n_eff.sum()
+        xyzs = xyzs.reshape(-1, 3)
+        dirs = dirs.reshape(-1, 3)
+        valid = ~torch.all(dirs == 0, dim=1)
+        if valid.sum() == 0:
+            break
+        sig = torch.zeros(xyzs.shape[0], device=dev)
+        col = torch.zeros(xyzs.shape[0], 3, device=dev)
+        s_v, c_v = call_model(xyzs[valid], dirs[valid])
+        sig[valid] = s_v.float()
+        col[valid] = c_v.float()
+        vren.composite_test_fw(sig.view(-1, step), col.view(-1, step, 3), deltas, ts, hits0,
+                               alive, kw.get("T_threshold", 1e-4), n_eff, opacity, depth, rgb)
+        alive = alive[alive >= 0]
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
+    return {"opacity": opacity, "depth": depth, "rgb": rgb + bg * (1 - opacity)[:, None],
+            "total_samples": total, "deltas": deltas}
+
+
+def render(model, rays_o, rays_d, **kwargs):
+    """rendering.py:12-46 for a single NGP model."""
+    with torch.autocast("cuda"):
+        rays_o, rays_d = rays_o.contiguous(), rays_d.contiguous()
+        hits_t = _near_far(model, rays_o, rays_d)
+        fn = _test_rays if kwargs.get("test_time", False) else _train_rays
+        call = lambda x, d: model(x, d)
+        res = fn(model, rays_o, rays_d, hits_t, model.density_bitfield, call, kwargs)
+        return _to_host(res, kwargs)
+
+
+def _to_host(res, kw):
+    if kw.get("to_cpu", False):
+        res = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in res.items()}
+        if kw.get("to_numpy", False):
+            res = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in res.items()}
+    return res
+
+
+def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):
+    """ml_rendering.py:11-78: gate, K sub-NeRF renders, gate-weighted combine."""
+    if kwargs.get("fused", False) and not kwargs.get("test_time", False):
+        from .fused import ml_render_fused
+        return ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup, **kwargs)
+    with torch.autocast("cuda"):
+        rays_o, rays_d = rays_o.contiguous(), rays_d.contiguous()
+        second = imgs_d.contiguous() if gating_net.type == "image" else rays_d
+        gate, importance, _ = gating_net(torch.cat((rays_o, second), 1), warmup)
+        B, K, dev = rays_o.shape[0], model.size, rays_o.device
+        rgb_acc = torch.zeros(B, 3, device=dev)
+        op_acc = torch.zeros(B, device=dev)
+        depth_all = torch.zeros(B, K, device=dev)
+        singles = []
+        noise = kwargs.pop("noise", None)
+        fn = _test_rays if kwargs.get("test_time", False) else _train_rays
+        for i in range(K):
+            hits_t = _near_far(model, rays_o, rays_d)
+            kw = dict(kwargs)
+            if noise is not None:
+                kw["noise"] = noise[i]
+            call = lambda x, d, i=i: model(x, d, i)
+            r = fn(model, rays_o, rays_d, hits_t, getattr(model, f"density_bitfield_{i}"), call, kw)
+            r = _to_host(r, kwargs)
+            singles.append(r["rgb"])
+            rgb_acc = rgb_acc + r["rgb"] * gate[:, i][:, None]
+            depth_all[:, i] = r["depth"]
+            op_acc = op_acc + r["opacity"] * gate[:, i]
+        return {"rgb": rgb_acc, "independent_rgbs": singles, "depth": depth_all,
+                "opacity": op_acc, "gating_code": gate, "gating_importance": importance}

@@ -1,0 +1,119 @@
+"""GPU parity of the fused field (hash grid + SH + geo/rgb MLP) and the ray gate
+against the torch-CPU fp32 oracle (oracle/field_oracle.py).
+
+The kernels run the MLPs on f16 MFMA with fp32 accumulation and round
+activations to f16 exactly where the oracle does (tcnn semantics), so the
+residual differences are fp32 summation order, occasionally flipping one f16
+ulp of an activation.  Tolerances (written per assertion):
+  forward sigma, rgb:   |diff| <= 5e-3 + 1e-2*|ref|, and 99th pct <= 1e-3-level
+  backward grads:       ||g - g_ref|| / ||g_ref|| <= 2e-2 (f16 backward chain)
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import field_oracle as fo
+from radnerf_amd import layout as LY
+from radnerf_amd import synthetic as S
+from radnerf_amd.networks import MNGP, Ray_Gate
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(cuda, scale=0.5, size=2):
+    m = MNGP(scale, size=size, seed=3)
+    with torch.no_grad():
+        m.xyz_encoder.params.copy_(torch.from_numpy(S.grid_params(m.xyz_encoder.n_entries)).view(-1))
+        m.mlp_params.copy_(torch.from_numpy(S.mlp_params(size, LY.FIELD_PARAMS)))
+    return m.to(cuda)
+
+
+def _inputs(n, scale, seed=9):
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(-scale * 1.02, scale * 1.02, (n, 3)).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    return x, d
+
+
+def _oracle_field(m, x, d, ind, scale):
+    lv = fo.grid_levels(scale)
+    gp = m.xyz_encoder.params.detach().cpu().view(-1, 2).half().float().requires_grad_(True)
+    mp = m.mlp_params.detach().cpu().clone().requires_grad_(True)
+    from oracle.ml_oracle import _split_field
+    sig, rgb = fo.field_forward(torch.from_numpy(x), torch.from_numpy(d), gp, _split_field(mp[ind]),
+                                lv, m.xyz_min.cpu(), m.xyz_max.cpu())
+    return sig, rgb, gp, mp
+
+
+def test_level_table_matches_oracle():
+    for scale in (0.5, 16.0):
+        a, b = LY.grid_levels(scale), fo.grid_levels(scale)
+        assert a["n_entries"] == b["n_entries"]
+        for k in ("offset", "hsize", "res"):
+            assert np.array_equal(a[k].astype(np.int64), b[k])
+        assert np.array_equal(a["scale"], b["scale"])
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_field_forward(cuda, scale):
+    m = _model(cuda, scale)
+    n = 5000
+    x, d = _inputs(n, scale)
+    for ind in range(2):
+        sig, rgb = m(torch.from_numpy(x).to(cuda), torch.from_numpy(d).to(cuda), ind)
+        osig, orgb, _, _ = _oracle_field(m, x, d, ind, scale)
+        sig, rgb = sig.detach().cpu().numpy(), rgb.detach().cpu().numpy()
+        osig, orgb = osig.detach().numpy(), orgb.detach().numpy()
+        e_rgb = np.abs(rgb - orgb)
+        e_sig = np.abs(sig - osig) / (1e-2 + np.abs(osig))
+        assert e_rgb.max() <= 5e-3, e_rgb.max()
+        assert np.percentile(e_rgb, 99) <= 1e-3
+        assert e_sig.max() <= 1e-2, e_sig.max()
+
+
+def test_field_backward(cuda):
+    scale = 0.5
+    m = _model(cuda, scale)
+    n = 4000
+    x, d = _inputs(n, scale, seed=4)
+    rng = np.random.default_rng(8)
+    ds = rng.normal(0, 1, n).astype(np.float32)
+    dr = rng.normal(0, 1, (n, 3)).astype(np.float32)
+    ind = 1
+    m.zero_grad()
+    sig, rgb = m(torch.from_numpy(x).to(cuda), torch.from_numpy(d).to(cuda), ind)
+    torch.autograd.backward([sig, rgb], [torch.from_numpy(ds).to(cuda), torch.from_numpy(dr).to(cuda)])
+    osig, orgb, gp, mp = _oracle_field(m, x, d, ind, scale)
+    torch.autograd.backward([osig, orgb], [torch.from_numpy(ds), torch.from_numpy(dr)])
+    g_grid = m.xyz_encoder.params.grad.cpu().view(-1, 2).numpy()
+    g_mlp = m.mlp_params.grad.cpu().numpy()
+    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+    assert rel(g_grid, gp.grad.numpy()) <= 2e-2, rel(g_grid, gp.grad.numpy())
+    assert rel(g_mlp[ind], mp.grad[ind].numpy()) <= 2e-2, rel(g_mlp[ind], mp.grad[ind].numpy())
+    assert np.abs(g_mlp[1 - ind]).max() == 0
+    for name, sl in LY.split_field_params(np.arange(LY.FIELD_PARAMS)).items():
+        idx = sl.reshape(-1)
+        assert rel(g_mlp[ind][idx], mp.grad[ind].numpy()[idx]) <= 3e-2, name
+
+
+@pytest.mark.parametrize("K", [2, 4, 8])
+def test_gate_forward_backward(cuda, K):
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6, scale=0.3)[0]))
+    g = g.to(cuda)
+    o, d = S.rays(3000)
+    x = np.concatenate([o, d], 1)
+    gate, imp, _ = g(torch.from_numpy(x).to(cuda))
+    from oracle.ml_oracle import _split_gate
+    gp = g.params.detach().cpu().clone().requires_grad_(True)
+    ogate = fo.gate_forward(torch.from_numpy(x), _split_gate(gp, K))
+    assert np.abs(gate.detach().cpu().numpy() - ogate.detach().numpy()).max() <= 2e-3
+    assert np.allclose(gate.sum(1).detach().cpu().numpy(), 1, atol=1e-5)
+    rng = np.random.default_rng(1)
+    dg = rng.normal(0, 1, (3000, K)).astype(np.float32)
+    gate.backward(torch.from_numpy(dg).to(cuda))
+    ogate.backward(torch.from_numpy(dg))
+    a, b = g.params.grad.cpu().numpy(), gp.grad.numpy()
+    assert np.linalg.norm(a - b) / np.linalg.norm(b) <= 2e-2

@@ -1,0 +1,122 @@
+"""End-to-end Rad-NeRF training render on the GPU: fused chain vs the drop-in
+(reference-structured) chain vs the CPU oracle (oracle/ml_oracle.py).
+
+Bars:
+  * fused march: per-(model, ray) sample counts and t / dt bit-exact vs oracle;
+  * fused vs drop-in GPU paths: outputs within 1e-5, gradients within 1e-3 rel
+    (same kernels; only float-atomic accumulation order differs);
+  * vs oracle: rgb / opacity / depth L_inf reported; rgb <= 1e-3 (the f16
+    field can flip one f16 ulp of an activation vs the fp32-ordered oracle;
+    the composite alone is held to 1e-4 in test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import ml_oracle
+from radnerf_amd import layout as LY
+from radnerf_amd import synthetic as S
+from radnerf_amd.fused import ml_render_fused, get_renderer
+from radnerf_amd.networks import MNGP, Ray_Gate
+from radnerf_amd.rendering import ml_render
+
+pytestmark = pytest.mark.gpu
+
+
+def _setup(cuda, B=384, K=2, scale=0.5, p=0.5):
+    m = MNGP(scale, size=K, seed=3)
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        m.xyz_encoder.params.copy_(torch.from_numpy(S.grid_params(m.xyz_encoder.n_entries)).view(-1))
+        m.mlp_params.copy_(torch.from_numpy(S.mlp_params(K, LY.FIELD_PARAMS)))
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6)[0]))
+        bits = S.bitfields(K, m.cascades, p=p)
+        for i in range(K):
+            getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    m, g = m.to(cuda), g.to(cuda)
+    o, d = S.rays(B, scale)
+    noise = S.noise(K, B)
+    seeds = S.loss_seeds(B, K)
+    return m, g, o, d, noise, seeds, bits
+
+
+def _run(fn, m, g, o, d, noise, seeds, cuda, esf):
+    m.zero_grad(); g.zero_grad()
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    res = fn(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=esf)
+    torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]], [to(s) for s in seeds])
+    grads = [m.xyz_encoder.params.grad.clone(), m.mlp_params.grad.clone(), g.params.grad.clone()]
+    return res, grads
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_fused_vs_dropin_vs_oracle(cuda, scale):
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, scale=scale)
+    rf, gf = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    rd, gd = _run(ml_render, m, g, o, d, noise, seeds, cuda, esf)
+    for k in ("rgb", "opacity", "depth", "gating_code"):
+        assert torch.allclose(rf[k], rd[k], atol=1e-5, rtol=0), k
+    for a, b in zip(gf, gd):
+        rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+        assert rel <= 1e-3, rel
+    ores = ml_oracle.ml_train_step(o, d, bits, noise, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                   m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale,
+                                   seeds=seeds)
+    # fused march bit-exact vs oracle, per (model, ray) segment
+    w = get_renderer(m, g, len(o)).ws
+    cnt = w.counts.cpu().numpy()
+    assert np.array_equal(cnt, ores["counts"])
+    off = w.offsets.cpu().numpy()
+    ts, dl = w.ts.cpu().numpy(), w.deltas.cpu().numpy()
+    K, B = cnt.shape
+    for k in range(K):
+        for r in range(0, B, 7):
+            a, c = off[k, r], ores["starts"][k, r]
+            n = cnt[k, r]
+            assert np.array_equal(ts[a:a + n].view(np.uint32), ores["ts"][c:c + n].view(np.uint32))
+            assert np.array_equal(dl[a:a + n].view(np.uint32), ores["deltas"][c:c + n].view(np.uint32))
+    e_rgb = np.abs(rf["rgb"].detach().cpu().numpy() - ores["rgb"]).max()
+    e_op = np.abs(rf["opacity"].detach().cpu().numpy() - ores["opacity"]).max()
+    e_de = np.abs(rf["depth"].detach().cpu().numpy() - ores["depth"]).max()
+    print(f"scale {scale}: rgb Linf {e_rgb:.2e} opacity {e_op:.2e} depth {e_de:.2e}")
+    assert e_rgb <= 1e-3 and e_op <= 1e-3 and e_de <= 1e-3 * max(1, scale)
+    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+    assert rel(gf[0].cpu().view(-1, 2).numpy(), ores["grid_grad"]) <= 5e-2
+    assert rel(gf[1].cpu().numpy(), ores["mlp_grad"]) <= 5e-2
+    assert rel(gf[2].cpu().numpy(), ores["gate_grad"]) <= 5e-2
+
+
+def test_fused_full_size_properties(cuda):
+    """BASELINE config C3 size (B=8192, K=2): size-independent properties."""
+    B, K = 8192, 2
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    res = ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
+    r = get_renderer(m, g, B)
+    w = r.ws
+    cnt = w.counts.cpu().numpy().astype(np.int64)
+    total = int(w.meta[1])
+    assert total == cnt.sum() and total > 1_000_000
+    assert cnt.max() <= 1024
+    # offsets: exclusive prefix per model, model bases aligned to 128
+    off = w.offsets.cpu().numpy().astype(np.int64)
+    base = w.seg_base.cpu().numpy()
+    for k in range(K):
+        assert base[k] % 128 == 0
+        assert np.array_equal(off[k], base[k] + np.concatenate([[0], np.cumsum(cnt[k])[:-1]]))
+    # t strictly increasing inside every segment (sampled rays)
+    ts = w.ts.cpu().numpy()
+    for k in range(K):
+        for rr in range(0, B, 97):
+            seg = ts[off[k, rr]:off[k, rr] + cnt[k, rr]]
+            assert np.all(np.diff(seg) > 0)
+    op = res["opacity"].detach().cpu().numpy()
+    assert np.all(op >= -1e-6) and np.all(op <= 1 + 1e-5)
+    gate = res["gating_code"].detach().cpu().numpy()
+    assert np.allclose(gate.sum(1), 1, atol=1e-5)
+    rgb = res["rgb"].detach().cpu().numpy()
+    assert np.all(np.isfinite(rgb)) and rgb.min() >= -1e-5 and rgb.max() <= 1 + 1e-4
+    # determinism of the forward (no atomics on the forward path)
+    res2 = ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
+    assert torch.equal(res["rgb"], res2["rgb"])
