@@ -1,0 +1,206 @@
+#!/usr/bin/env python
+"""Headline benchmark: million samples/s fwd+bwd of the Rad-NeRF hot path.
+
+Workload (BASELINE.json configs[2], "C3"): Rad-NeRF train_ml.py with
+model_zoo_size K=2, gate_type=ray, B=8192 rays per GPU, scale 0.5 (1 cascade,
+exp_step_factor 0), on synthetic rays through a random-init 128^3 occupancy
+grid (Bernoulli p=0.5 per cell, one grid per sub-NeRF) and random-init
+parameters (tcnn-style: hash table U(-1e-4,1e-4), Xavier MLPs).
+A step = gate fwd + K x (AABB + march + field fwd + composite fw) + gated
+combine, then the full backward (combine bw, composite bw, field bw with hash
+grid + MLP weight gradients, gate bw) seeded with N(0,1e-3) loss gradients;
+at N>1 plus one RCCL all-reduce of all gradients (weak scaling: every rank
+renders its own 8192 rays).  Optimizer / density-grid update excluded, as in
+the metric definition.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "rad-nerf_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "million samples/s fwd+bwd, 8192 rays, model_zoo_size=2; rgb L∞ vs ref"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+# algorithmic bytes per sample of the field backward kernel:
+#   dL/dsigma + dL/drgb read 16 + sample position/direction re-read 24 +
+#   hash-grid gradient scatter 1024 (16 levels x 8 corners x 2 fp32) = 1064 B
+FIELD_BWD_BYTES_PER_SAMPLE = 16 + 24 + 1024
+# field forward: read 24 + hash gather 512 + sigma/rgb write 16
+FIELD_FWD_BYTES_PER_SAMPLE = 24 + 512 + 16
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rays", type=int, default=8192, help="rays per GPU")
+    ap.add_argument("--models", type=int, default=2)
+    ap.add_argument("--scale", type=float, default=0.5)
+    ap.add_argument("--occupancy", type=float, default=0.5)
+    ap.add_argument("--cpu-rays", type=int, default=512,
+                    help="rays in the bounded CPU-oracle sample: CPU baseline timing and the "
+                         "rgb L_inf check (0 = skip)")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    from radnerf_amd import dist as rdist
+    from radnerf_amd import synthetic as S
+    from radnerf_amd.fused import FusedMLRenderer
+    from radnerf_amd.networks import MNGP, Ray_Gate
+
+    rank, local, world = rdist.init()
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs a GPU")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B, K, scale = args.rays, args.models, args.scale
+    esf = 1.0 / 256 if scale > 0.5 else 0.0
+
+    model = MNGP(scale, size=K, seed=3).to(dev)
+    gate = Ray_Gate(K, seed=4).to(dev)
+    bits = S.bitfields(K, model.cascades, p=args.occupancy, seed=1)
+    with torch.no_grad():
+        for i in range(K):
+            getattr(model, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    o_np, d_np = S.rays(B, scale, seed=1000 * rank)
+    rays_o = torch.from_numpy(o_np).to(dev)
+    rays_d = torch.from_numpy(d_np).to(dev)
+    noises = [torch.from_numpy(S.noise(K, B, seed=2 + 7919 * rank + i)).to(dev) for i in range(4)]
+    seeds_np = S.loss_seeds(B, K, seed=4 + rank)
+    g_rgb, g_op, g_depth = (torch.from_numpy(s).to(dev) for s in seeds_np)
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
+
+    r = FusedMLRenderer(model, gate, B)
+    ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
+    samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
+
+    def step(i):
+        ar.zero()
+        _, _, _, gt, _ = r.forward(rays_o, rays_d, rays_d, noises[i % 4], bg, 1e-4, esf)
+        samples_acc.add_(r.ws.meta[1])
+        r.backward(rays_o, rays_d, rays_d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4,
+                   grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
+        if world > 1:
+            ar.reduce()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    samples_acc.zero_()
+    r.trace = True
+    r.events = {}
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    r.trace = False
+    kt = r.kernel_times_ms()
+    n_samples = samples_acc.clone()
+    t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(n_samples)
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+    elapsed = float(t_max)
+    total_samples = int(n_samples)
+    value = total_samples / elapsed / 1e6
+
+    # per-kernel breakdown (rank 0) and the roofline of the dominant kernel
+    kms = {k: float(np.mean(v)) for k, v in kt.items()}
+    samples_per_step_rank = int(samples_acc) / args.steps
+    bwd_ms = kms.get("field_bwd", float("nan"))
+    achieved = samples_per_step_rank * FIELD_BWD_BYTES_PER_SAMPLE / (bwd_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            traffic = tj.get("field_bwd_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+    roofline = {"kernel": "field_bwd", "bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "algorithmic_bytes_per_sample": FIELD_BWD_BYTES_PER_SAMPLE,
+                "samples_per_launch": round(samples_per_step_rank),
+                "avg_launch_ms": round(bwd_ms, 4)}
+
+    rgb_linf = None
+    cpu_base = None
+    if rank == 0 and world == 1 and args.cpu_rays > 0:
+        rgb_linf, cpu_base = oracle_legs(args, model, gate, bits, o_np, d_np, noises[0], r,
+                                         rays_o, rays_d, bg, esf, scale, seeds_np)
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "f16/f32",
+               "data": "synthetic",
+               "config": {"workload": "C3 Rad-NeRF train_ml.py K=2 gate=ray B=8192/GPU "
+                                      "scale=0.5, random 128^3 occupancy p=%.2f" % args.occupancy,
+                          "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,
+                          "samples_per_step_per_gpu": round(samples_per_step_rank),
+                          "global_batch": B * world, "parallelism": f"dp{world}"},
+               "roofline": roofline, "cpu_baseline": cpu_base,
+               "rgb_linf_vs_ref": rgb_linf,
+               "kernel_ms": {k: round(v, 4) for k, v in sorted(kms.items())}}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, bg, esf, scale,
+                seeds_np):
+    """rgb L_inf of the GPU path vs the CPU oracle on the first rays of the
+    workload, and the CPU-oracle throughput on a bounded sample."""
+    from oracle import ml_oracle
+    n = args.cpu_rays
+    rgb, _, _, _, _ = r.forward(rays_o, rays_d, rays_d, noise, bg, 1e-4, esf)
+    rgb = rgb.cpu().numpy()
+    gp = model.xyz_encoder.params.detach().cpu().view(-1, 2).numpy()
+    mp = model.mlp_params.detach().cpu().numpy()
+    ap = gate.params.detach().cpu().numpy()
+    nz = noise.cpu().numpy()
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    # one bounded oracle step (fwd + bwd) serves both legs: its forward rgb is
+    # compared with the GPU's rgb for the same rays, its wall time is the baseline
+    c = n
+    sd = tuple(np.ascontiguousarray(s[:c]) for s in seeds_np)
+    t0 = time.perf_counter()
+    res = ml_oracle.ml_train_step(o_np[:c], d_np[:c], bits, np.ascontiguousarray(nz[:, :c]),
+                                  gp, mp, ap, scale, seeds=sd)
+    dt = time.perf_counter() - t0
+    rgb_linf = float(np.abs(res["rgb"] - rgb[:c]).max())
+    cpu = {"value": round(res["total"] / dt / 1e6, 5), "unit": "Msamples/s",
+           "cores": threads, "kind": "port",
+           "sample": f"{c} rays x K={args.models} ({res['total']} samples) of the same workload, "
+                     f"one fwd+bwd step of oracle/ml_oracle.py (C march/composite + torch-CPU "
+                     f"fp32 field, {threads} threads), {dt:.1f} s"}
+    return rgb_linf, cpu
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,77 @@
+"""Ray-batch data parallelism: one process per GPU, each rank
+renders its own ray batch with full replicas of the hash grid, the K sub-NeRF
+MLPs, the gate and all K occupancy bitfields; gradients are summed with one
+RCCL all-reduce over xGMI per step (torch.distributed backend "nccl" = RCCL
+on ROCm; "gloo" for the CPU tests).
+
+The reference is single-GPU (train_ml.py:295-304); this is the build's
+addition.  Bitfields must stay identical across ranks: `broadcast_buffers`
+ships rank 0's copy (C x 256 KiB per sub-NeRF) after a density-grid update.
+"""
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def init(backend=None):
+    """Initialise the default process group from the torchrun env (no-op for 1 rank)."""
+    rank, local, world = env_rank()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return rank, local, world
+
+
+def shard_rays(n_total, rank, world):
+    """Contiguous ray range of this rank for a global batch of n_total rays."""
+    per = (n_total + world - 1) // world
+    lo = min(rank * per, n_total)
+    return lo, min(lo + per, n_total)
+
+
+class GradAllReduce:
+    """Flat-buffer gradient all-reduce (mean over ranks).
+
+    All gradient tensors are views of one contiguous fp32 buffer, so a step
+    issues a single large collective (45.7 MB hash-grid gradient + MLP/gate
+    gradients at scale 0.5) instead of one per parameter."""
+
+    def __init__(self, params, device):
+        self.params = list(params)
+        sizes = [p.numel() for p in self.params]
+        self.flat = torch.zeros(sum(sizes), device=device)
+        self.views = []
+        off = 0
+        for p, n in zip(self.params, sizes):
+            self.views.append(self.flat[off:off + n].view_as(p))
+            off += n
+
+    def zero(self):
+        self.flat.zero_()
+
+    def reduce(self, average=True):
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            dist.all_reduce(self.flat)
+            if average:
+                self.flat.div_(dist.get_world_size())
+        return self.views
+
+
+def broadcast_buffers(module, src=0):
+    """Keep density grids / bitfields identical across ranks."""
+    if dist.is_initialized() and dist.get_world_size() > 1:
+        for name, b in module.named_buffers():
+            if "density" in name:
+                dist.broadcast(b, src)

@@ -83,6 +83,24 @@ class FusedMLRenderer:
         self.bitfield_bytes = bf[0].numel()
         self.fwd_blocks = fwd_blocks or max(1, 2048 // K)
         self.bwd_blocks = bwd_blocks or max(1, 256 // K)
+        self.trace = False          # record HIP events around every launch
+        self.events = {}
+
+    def _ev(self, name, L_call, *args):
+        """Launch through librn; with tracing on, bracket it with events on the
+        launch stream (bench.py's per-kernel timing)."""
+        if not self.trace:
+            return L_call(*args)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        L_call(*args)
+        b.record()
+        self.events.setdefault(name, []).append((a, b))
+
+    def kernel_times_ms(self):
+        """{kernel: [ms per launch]} of the traced launches (synchronises)."""
+        torch.cuda.synchronize()
+        return {k: [a.elapsed_time(b) for a, b in v] for k, v in self.events.items()}
 
     def bitfields(self):
         K = self.model.size
@@ -101,27 +119,30 @@ class FusedMLRenderer:
         st = _stream(rays_o.device)
         out_gate = torch.empty(B, K, device=rays_o.device)
         imp = torch.zeros(K, device=rays_o.device)
-        L.gate_fwd(rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K, g.packed_frags().data_ptr(),
-                   out_gate.data_ptr(), imp.data_ptr(), max(1, min(256, (B + 127) // 128)), st)
+        self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
+                 g.packed_frags().data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
+                 max(1, min(256, (B + 127) // 128)), st)
         bits = self.bitfields()
         march = (rays_o.data_ptr(), rays_d.data_ptr(), m.center.data_ptr(),
                  m.half_size.data_ptr(), NEAR_DISTANCE, noise.data_ptr(), bits.data_ptr(),
                  self.bitfield_bytes, K, m.cascades, float(m.scale), float(exp_step_factor),
                  m.grid_size, MAX_SAMPLES, B)
-        L.ml_march_count(*march, w.counts.data_ptr(), st)
-        L.scan_segments(w.counts.data_ptr(), K, B, SEG_ALIGN, w.offsets.data_ptr(),
-                        w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.meta.data_ptr(), st)
-        L.ml_march_write(*march, w.counts.data_ptr(), w.offsets.data_ptr(), w.ts.data_ptr(),
-                         w.deltas.data_ptr(), w.ray_of.data_ptr(), st)
+        self._ev("march_count", L.ml_march_count, *march, w.counts.data_ptr(), st)
+        self._ev("scan", L.scan_segments, w.counts.data_ptr(), K, B, SEG_ALIGN,
+                 w.offsets.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(),
+                 w.meta.data_ptr(), st)
+        self._ev("march_write", L.ml_march_write, *march, w.counts.data_ptr(),
+                 w.offsets.data_ptr(), w.ts.data_ptr(), w.deltas.data_ptr(), w.ray_of.data_ptr(),
+                 st)
         self._field(True, rays_o, rays_d, st)
-        L.ml_composite_fw(w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
+        self._ev("composite_fw", L.ml_composite_fw, w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
                           w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
                           float(T_threshold), w.used.data_ptr(), w.opacity_k.data_ptr(),
                           w.depth_k.data_ptr(), w.rgb_k.data_ptr(), w.ws.data_ptr(), st)
         rgb = torch.empty(B, 3, device=rays_o.device)
         opacity = torch.empty(B, device=rays_o.device)
         depth = torch.empty(B, K, device=rays_o.device)
-        L.ml_combine_fw(out_gate.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
+        self._ev("combine_fw", L.ml_combine_fw, out_gate.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
                         w.rgb_k.data_ptr(), bg.data_ptr(), B, K, rgb.data_ptr(),
                         opacity.data_ptr(), depth.data_ptr(), st)
         return rgb, opacity, depth, out_gate, imp
@@ -134,9 +155,11 @@ class FusedMLRenderer:
                   m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
         if fwd:
-            L.field_fwd(*common, w.sigma.data_ptr(), w.rgb.data_ptr(), self.fwd_blocks, st)
+            self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
+                     self.fwd_blocks, st)
         else:
-            L.field_bwd(*common, m.dw_map(rays_o.device).data_ptr(), w.dsigma.data_ptr(),
+            self._ev("field_bwd", L.field_bwd, *common, m.dw_map(rays_o.device).data_ptr(),
+                     w.dsigma.data_ptr(),
                         w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(), self.bwd_blocks,
                         st)
 
@@ -153,11 +176,11 @@ class FusedMLRenderer:
         grid_grad = torch.zeros_like(m.xyz_encoder.params) if grid_grad is None else grid_grad
         mlp_grad = torch.zeros_like(m.mlp_params) if mlp_grad is None else mlp_grad
         gate_grad = torch.zeros_like(g.params) if gate_grad is None else gate_grad
-        L.ml_combine_bw(dL_drgb.data_ptr(), dL_dopacity.data_ptr(), w.opacity_k.data_ptr(),
+        self._ev("combine_bw", L.ml_combine_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(), w.opacity_k.data_ptr(),
                         w.rgb_k.data_ptr(), bg.data_ptr(), B, K, w.dgate.data_ptr(), st)
         if dL_dgate_ext is not None:
             w.dgate.add_(dL_dgate_ext)
-        L.ml_composite_bw(dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
+        self._ev("composite_bw", L.ml_composite_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
                           None if dL_ddepth is None else dL_ddepth.data_ptr(), gate.data_ptr(),
                           bg.data_ptr(), w.sigma.data_ptr(), w.rgb.data_ptr(),
                           w.deltas.data_ptr(), w.ts.data_ptr(), w.counts.data_ptr(),
@@ -165,7 +188,8 @@ class FusedMLRenderer:
                           w.rgb_k.data_ptr(), B, K, float(T_threshold), w.dsigma.data_ptr(),
                           w.drgb.data_ptr(), st)
         self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
-        L.gate_bwd(rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K, g.packed_frags().data_ptr(),
+        self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
+                 g.packed_frags().data_ptr(),
                    g.dw_map(dev).data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
                    gate_grad.numel(), max(1, min(128, (B + 127) // 128)), st)
         return grid_grad, mlp_grad, gate_grad
