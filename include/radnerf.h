@@ -21,6 +21,8 @@ extern "C" {
 
 int rn_version(void);
 const char* rn_last_error(void);
+/* ablation switches for kernel studies (tools/ablate.py); 0 = production */
+void rn_set_debug_flags(int flags);
 
 /* ---- ray / AABB -----------------------------------------------------------
  * replaces vren.ray_aabb_intersect  (models/csrc/binding.cpp:4-16,

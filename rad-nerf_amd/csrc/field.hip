@@ -27,6 +27,9 @@
 #define FIELD_FRAGS 46
 #define FIELD_PARAMS 9472
 #define FIELD_DW_TILES 12
+#ifndef FWD_MIN_WAVES
+#define FWD_MIN_WAVES 3
+#endif
 
 struct GridMeta {
     uint32_t offset[RN_L];  // level offset in entries (1 entry = 2 halfs)
@@ -34,6 +37,7 @@ struct GridMeta {
     uint32_t res[RN_L];     // grid resolution
     float scale[RN_L];      // tcnn grid_scale (host-computed fp32)
     uint32_t dense_mask;    // bit l set: dense indexing
+    uint32_t pow2_mask;     // bit l set: hsize is a power of two
 };
 
 struct FieldArgs {
@@ -50,8 +54,12 @@ struct FieldArgs {
     float* sigma; float* rgb; // forward outputs
     const float* dsigma; const float* drgb;               // backward seeds
     float xyz_min[3]; float extent[3];
+    uint32_t grid_bytes;      // byte size of the f16 table (= of the f32 grad / 2)
+    int dbg;                  // ablation flags (rn_set_debug_flags), 0 in production
     GridMeta gm;
 };
+
+static int g_field_dbg = 0;
 
 namespace {
 
@@ -86,17 +94,34 @@ __device__ __forceinline__ float unit_coord(float v, float mn, float ext) {
 
 __device__ __forceinline__ int lane_level(int q, int h) { return 2 * h + (q & 1) + 4 * (q >> 1); }
 
-// tcnn grid_index (Linear, coherent prime hash)
-__device__ __forceinline__ uint32_t grid_index(const GridMeta& gm, int l, uint32_t x, uint32_t y,
-                                               uint32_t z) {
+// Level table staged in LDS: lanes index it with a lane-dependent level, which
+// from the kernel-argument segment would be a global load per access.
+struct LvTab {
+    uint32_t off[RN_L];
+    uint32_t hs[RN_L];
+    uint32_t res[RN_L];
+    float sc[RN_L];
+};
+
+__device__ __forceinline__ void lv_stage(LvTab& t, const GridMeta& gm) {
+    const int i = threadIdx.x;
+    if (i < RN_L) {
+        t.off[i] = gm.offset[i]; t.hs[i] = gm.hsize[i]; t.res[i] = gm.res[i]; t.sc[i] = gm.scale[i];
+    }
+}
+
+// tcnn grid_index (Linear, coherent prime hash); masks are wave-uniform SGPRs
+__device__ __forceinline__ uint32_t grid_index(const LvTab& T, const GridMeta& gm, int l,
+                                               uint32_t x, uint32_t y, uint32_t z) {
     uint32_t idx;
     if ((gm.dense_mask >> l) & 1u) {
-        const uint32_t r = gm.res[l];
+        const uint32_t r = T.res[l];
         idx = x + y * r + z * r * r;
     } else {
         idx = x ^ (y * 2654435761u) ^ (z * 805459861u);
     }
-    const uint32_t hs = gm.hsize[l];
+    const uint32_t hs = T.hs[l];
+    if ((gm.pow2_mask >> l) & 1u) return idx & (hs - 1u);   // hashed levels: T = 2^k
     return idx < hs ? idx : idx % hs;
 }
 
@@ -119,33 +144,56 @@ __device__ __forceinline__ float corner_weight(const LevelPos& p, int c) {
     return w;
 }
 
-// hash-grid encoding of this lane's 8 levels -> the two B fragments
-__device__ __forceinline__ void encode_lane(const FieldArgs& a, int h, float ux, float uy, float uz,
-                                            bool valid, half8& e0, half8& e1) {
-    const uint32_t* g32 = reinterpret_cast<const uint32_t*>(a.grid);
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rn_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes,
+                                             0x00020000);
+}
+
+#define RN_OOB 0x80000000u   // buffer offset past num_records: load returns 0
+
+// hash-grid encoding of this lane's 8 levels -> the two B fragments.
+// Two levels (16 corner gathers) in flight per batch, 32-bit buffer offsets;
+// invalid lanes read out of range (hardware returns zero).
+__device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
+                                            __amdgpu_buffer_rsrc_t rs, int h, float ux, float uy,
+                                            float uz, bool valid, half8& e0, half8& e1) {
     float f[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int l = lane_level(q, h);
-        const LevelPos p = level_pos(a.gm.scale[l], ux, uy, uz);
-        float a0 = 0.f, a1 = 0.f;
-        uint32_t raw[8];
+    for (int qb = 0; qb < 8; qb += 2) {
+        LevelPos P[2];
+        uint32_t off[16];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const uint32_t idx = grid_index(a.gm, l, p.gx + (c & 1), p.gy + ((c >> 1) & 1),
-                                            p.gz + ((c >> 2) & 1));
-            raw[c] = valid ? g32[a.gm.offset[l] + idx] : 0u;
-        }
+        for (int u = 0; u < 2; ++u) {
+            const int l = lane_level(qb + u, h);
+            P[u] = level_pos(T.sc[l], ux, uy, uz);
+            const uint32_t lo = T.off[l];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            const float w = corner_weight(p, c);
-            const uint32_t v = raw[c];
-            const rn_half v0 = __builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu));
-            const rn_half v1 = __builtin_bit_cast(rn_half, (uint16_t)(v >> 16));
-            a0 = fmaf(w, (float)v0, a0);
-            a1 = fmaf(w, (float)v1, a1);
+            for (int c = 0; c < 8; ++c) {
+                const uint32_t idx = grid_index(T, a.gm, l, P[u].gx + (c & 1),
+                                                P[u].gy + ((c >> 1) & 1), P[u].gz + ((c >> 2) & 1));
+                off[8 * u + c] = valid ? 4u * (lo + idx) : RN_OOB;
+            }
         }
-        f[2 * q] = a0; f[2 * q + 1] = a1;
+        uint32_t raw[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) raw[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i], 0, 0);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const float w = corner_weight(P[u], c);
+                const uint32_t v = raw[8 * u + c];
+                const rn_half v0 = __builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu));
+                const rn_half v1 = __builtin_bit_cast(rn_half, (uint16_t)(v >> 16));
+                a0 = fmaf(w, (float)v0, a0);
+                a1 = fmaf(w, (float)v1, a1);
+            }
+            f[2 * (qb + u)] = a0; f[2 * (qb + u) + 1] = a1;
+        }
+        // keep at most one batch of gathers in flight per wave: bounds VGPRs so
+        // more waves fit (TLP hides the L2/MALL latency instead of ILP)
+        __builtin_amdgcn_sched_barrier(0);
     }
     // element j of k-step s <-> level lane_level(4s + (j>>1), h), feature j&1
 #pragma unroll
@@ -234,9 +282,10 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
 template <int MODE>
-__device__ __forceinline__ void tile_forward(const FieldArgs& a, const rn_half* W, int64_t base,
-                                             int64_t n, int64_t tile, FwdState& st, bool& valid,
-                                             int64_t& s, float& ux, float& uy, float& uz) {
+__device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T, const rn_half* W,
+                                             int64_t base, int64_t n, int64_t tile, FwdState& st,
+                                             bool& valid, int64_t& s, float& ux, float& uy,
+                                             float& uz) {
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     const int64_t i = tile * 32 + c;
     valid = i < n;
@@ -246,18 +295,20 @@ __device__ __forceinline__ void tile_forward(const FieldArgs& a, const rn_half* 
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-    encode_lane(a, h, ux, uy, uz, valid, st.e0, st.e1);
+    encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
     st.sh = sh_lane(dx, dy, dz, h);
     mlp_forward(W, st);
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256, FWD_MIN_WAVES)
 k_field_fwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FWD_FRAGS * RN_FRAG_HALFS];
+    __shared__ LvTab sT;
     const int k = blockIdx.y;
     rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                     FIELD_FWD_FRAGS * RN_FRAG_BYTES);
+    lv_stage(sT, a.gm);
     __syncthreads();
     int64_t base, n;
     sample_range(a, MODE, k, base, n);
@@ -266,9 +317,10 @@ k_field_fwd(FieldArgs a) {
     const int lane = rn_lane(), h = lane >> 5;
     for (int64_t tile = (int64_t)blockIdx.x * waves + threadIdx.x / RN_WAVE; tile < n_tiles;
          tile += (int64_t)gridDim.x * waves) {
+        rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
         FwdState st;
         bool valid; int64_t s; float ux, uy, uz;
-        tile_forward<MODE>(a, sW, base, n, tile, st, valid, s, ux, uy, uz);
+        tile_forward<MODE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
         if (valid && h == 0) {
             // TruncExp.forward on the f16 geo output (custom_functions.py:165-167)
             a.sigma[s] = expf(st.g0);
@@ -280,68 +332,126 @@ k_field_fwd(FieldArgs a) {
     }
 }
 
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+// ---------------------------------------------------------------------------
+// Backward.  A block = 8 waves = 256 samples per iteration (one 32-sample tile
+// per wave), one model per blockIdx.y, persistent over iterations.
+// Weight gradients need a contraction over samples; instead of per-wave LDS
+// float atomics (measured ~5.8 ms per step: ds_add_f32 throughput), every
+// wave publishes its (dY, X) layer images in LDS and the 12 dW tiles are
+// OWNED by waves (1-2 each), which contract over all 256 samples of the block
+// (16 MFMAs per tile) into register accumulators that persist across
+// iterations and are flushed once with global atomics at the end.
+// Gradient scale: one power of two per block iteration (max over the 8 waves'
+// seeds); accumulators are rescaled exactly when it changes.
+// ---------------------------------------------------------------------------
+#define BWD_WAVES 8
+
+// dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
+__device__ __forceinline__ f32x16 dw_block_tile(const rn_half* sImg, int ya, int xa, f32x16 acc) {
+#pragma unroll
+    for (int w = 0; w < BWD_WAVES; ++w) {
+        const rn_half* iy = sImg + w * 2 * RN_IMG_HALFS;
+        const rn_half* ix = iy + RN_IMG_HALFS;
+        acc = rn_mfma(rn_img_read(iy, ya, 0), rn_img_read(ix, xa, 0), acc);
+        acc = rn_mfma(rn_img_read(iy, ya, 1), rn_img_read(ix, xa, 1), acc);
+    }
+    return acc;
 }
 
-// backward: 8 waves per block, one model per blockIdx.y, persistent tiles
-#define BWD_WAVES 8
-#define STG_HALFS (64 * RN_STG_STRIDE)   // 64 rows x 40 halfs = 5 KiB per wave
+// flush one owned dW tile (accumulated at scale `sc`) into the global gradient
+template <int MODE>
+__device__ __forceinline__ void dw_flush(const f32x16& acc, float* dw, int off, int ncols,
+                                         int out_base, int in_base, float inv) {
+    const int lane = rn_lane(), col = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        int out;
+        if (MODE == DW_PLAIN) out = out_base + row;
+        else if (MODE == DW_ROWS_LT3) out = row < 3 ? row : -1;
+        else out = row < 16 ? row + 1 : (row == 16 ? 0 : -1);
+        if (out >= 0) atomicAdd(dw + off + out * ncols + in_base + col, acc[i] * inv);
+    }
+}
 
 template <int MODE>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
 k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
-    __shared__ __attribute__((aligned(16))) float sDW[FIELD_PARAMS];
-    __shared__ __attribute__((aligned(16))) rn_half sStg[BWD_WAVES * STG_HALFS];
+    __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
+    __shared__ float sMax[BWD_WAVES];
+    __shared__ LvTab sT;
     const int k = blockIdx.y;
     rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                     FIELD_FRAGS * RN_FRAG_BYTES);
-    for (int i = threadIdx.x; i < FIELD_PARAMS; i += blockDim.x) sDW[i] = 0.f;
+    lv_stage(sT, a.gm);
     __syncthreads();
 
     int64_t base, n;
     sample_range(a, MODE, k, base, n);
     const int64_t n_tiles = (n + 31) / 32;
-    const int wid = threadIdx.x / RN_WAVE;
+    const int64_t n_iters = (n_tiles + BWD_WAVES - 1) / BWD_WAVES;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
-    rn_half* stg = sStg + wid * STG_HALFS;
+    rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
+    rn_half* imgX = imgY + RN_IMG_HALFS;
     const half8 z8 = rn_zero8();
+    const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
+    const bool do_dw = !(a.dbg & 2);
 
-    for (int64_t tile = (int64_t)blockIdx.x * BWD_WAVES + wid; tile < n_tiles;
-         tile += (int64_t)gridDim.x * BWD_WAVES) {
+    // owned dW tiles (ownership table in the header comment above):
+    //   w0: r3(n=0), g2(n=0)   w1: r3(n=1), g2(n=1)   w2..w5: r2(m,n)
+    //   w2: + g1(m=0)          w3: + g1(m=1)          w6, w7: r1(m)
+    f32x16 accA = rn_zero16(), accB = rn_zero16();
+    float cur_scale = 0.f;   // scale the accumulators are expressed at (0 = empty)
+
+    for (int64_t it = blockIdx.x; it < n_iters; it += gridDim.x) {
+        rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
+        const int64_t tile = it * BWD_WAVES + wid;
         FwdState st;
         bool valid; int64_t s; float ux, uy, uz;
-        tile_forward<MODE>(a, sW, base, n, tile, st, valid, s, ux, uy, uz);
+        tile_forward<MODE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
 
-        // ---- seeds: dL/dsigma, dL/drgb (lanes h == 0 own the output rows)
-        float ds = 0.f, dr0 = 0.f, dr1 = 0.f, dr2 = 0.f;
-        if (valid && h == 0) {
-            ds = a.dsigma[s];
-            dr0 = a.drgb[3 * s]; dr1 = a.drgb[3 * s + 1]; dr2 = a.drgb[3 * s + 2];
-        }
-        // sigmoid' = y(1-y); dO rows 0..2 (k-step 0 elements 0..2 of lanes h == 0)
-        half8 dO = z8;
+        // ---- seeds (lanes h == 0 own the output rows)
         float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
-        if (h == 0) {
+        if (valid && h == 0) {
+            const float ds = a.dsigma[s];
             const float y0 = sigmoidf(st.out[0]), y1 = sigmoidf(st.out[1]),
                         y2 = sigmoidf(st.out[2]);
-            o0 = dr0 * (y0 * (1.0f - y0));
-            o1 = dr1 * (y1 * (1.0f - y1));
-            o2 = dr2 * (y2 * (1.0f - y2));
+            o0 = a.drgb[3 * s] * (y0 * (1.0f - y0));        // sigmoid'
+            o1 = a.drgb[3 * s + 1] * (y1 * (1.0f - y1));
+            o2 = a.drgb[3 * s + 2] * (y2 * (1.0f - y2));
             // TruncExp.backward: g * exp(clamp(x, -15, 15))  (custom_functions.py:171-173)
             gsig = ds * expf(fminf(fmaxf(st.g0, -15.f), 15.f));
         }
-        const float gscale = rn_wave_grad_scale(
-            fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(gsig))));
-        const float ginv = 1.0f / gscale;
+        float m = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(gsig)));
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        if (lane == 0) sMax[wid] = m;
+        __syncthreads();                                                    // B0
+        float bm = sMax[0];
+#pragma unroll
+        for (int w = 1; w < BWD_WAVES; ++w) bm = fmaxf(bm, sMax[w]);
+        const float gscale = rn_wave_grad_scale(bm);   // uniform over the block
+        if (cur_scale != gscale) {                     // exact power-of-two rescale
+            const float r = cur_scale == 0.f ? 0.f : gscale / cur_scale;
+            accA *= r; accB *= r;
+            cur_scale = gscale;
+        }
+        half8 dO = z8;
         if (h == 0) {
             dO[0] = (rn_half)(o0 * gscale);
             dO[1] = (rn_half)(o1 * gscale);
             dO[2] = (rn_half)(o2 * gscale);
         }
-        // ---- dR2 = Wr3^T dO, masked by R2 > 0
+        // ---- layer rgb3: dW (w0, w1) = dO x R2 ; dR2 = Wr3^T dO masked
+        if (do_dw) {
+            rn_img_write(imgY, 0, dO); rn_img_write(imgY, 1, z8);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.r2[q]);
+        }
+        __syncthreads();                                                    // B1
+        if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
         half8 dr2f[4];
         {
             f32x16 b0 = rn_zero16(), b1 = rn_zero16();
@@ -350,7 +460,15 @@ k_field_bwd(FieldArgs a) {
             rn_acc_to_frags_masked(b0, st.r2[0], st.r2[1], dr2f[0], dr2f[1]);
             rn_acc_to_frags_masked(b1, st.r2[2], st.r2[3], dr2f[2], dr2f[3]);
         }
-        // ---- dR1 = Wr2^T dR2, masked by R1 > 0
+        __syncthreads();                                                    // B2
+        // ---- layer rgb2: dW (w2..w5) = dR2 x R1 ; dR1 = Wr2^T dR2 masked
+        if (do_dw) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { rn_img_write(imgY, q, dr2f[q]); rn_img_write(imgX, q, st.r1[q]); }
+        }
+        __syncthreads();                                                    // B3
+        if (do_dw && wid >= 2 && wid < 6)
+            accA = dw_block_tile(sImg, 32 * ((wid - 2) >> 1), 32 * ((wid - 2) & 1), accA);
         half8 dr1f[4];
         {
             f32x16 b0 = rn_zero16(), b1 = rn_zero16();
@@ -362,16 +480,32 @@ k_field_bwd(FieldArgs a) {
             rn_acc_to_frags_masked(b0, st.r1[0], st.r1[1], dr1f[0], dr1f[1]);
             rn_acc_to_frags_masked(b1, st.r1[2], st.r1[3], dr1f[2], dr1f[3]);
         }
-        // ---- dG (geo outputs 1..16) = Wr1[:,16:]^T dR1 ; row 16 = dL/dh0
+        __syncthreads();                                                    // B4
+        // ---- layer rgb1: dW (w6, w7) = dR1 x [SH | geo 1..16] ; dG
+        if (do_dw) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dr1f[q]);
+            rn_img_write(imgX, 0, st.sh); rn_img_write(imgX, 1, st.gin);
+        }
+        __syncthreads();                                                    // B5
+        if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
         half8 dg0, dg1;
         {
             f32x16 b = rn_zero16();
 #pragma unroll
             for (int q = 0; q < 4; ++q) b = rn_mfma(rn_frag(sW, 34 + q), dr1f[q], b);
-            if (h == 0) b[8] = gsig * gscale;
+            if (h == 0) b[8] = gsig * gscale;          // row 16 = dL/dh0
             rn_acc_to_frags<false>(b, dg0, dg1);
         }
-        // ---- dH1 = Wg2^T dG, masked by H1 > 0
+        __syncthreads();                                                    // B6
+        // ---- layer geo2: dW (w0, w1) = dG x H1 ; dH1 = Wg2^T dG masked
+        if (do_dw) {
+            rn_img_write(imgY, 0, dg0); rn_img_write(imgY, 1, dg1);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h1[q]);
+        }
+        __syncthreads();                                                    // B7
+        if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
         half8 dh1f[4];
         {
             f32x16 b0 = rn_zero16(), b1 = rn_zero16();
@@ -380,102 +514,87 @@ k_field_bwd(FieldArgs a) {
             rn_acc_to_frags_masked(b0, st.h1[0], st.h1[1], dh1f[0], dh1f[1]);
             rn_acc_to_frags_masked(b1, st.h1[2], st.h1[3], dh1f[2], dh1f[3]);
         }
-        // ---- dE = Wg1^T dH1  (rows = encoding features, natural order)
+        __syncthreads();                                                    // B8
+        // ---- layer geo1: dW (w2, w3) = dH1 x E ; dE = Wg1^T dH1
+        if (do_dw) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dh1f[q]);
+            rn_img_write(imgX, 0, st.e0); rn_img_write(imgX, 1, st.e1);
+        }
+        __syncthreads();                                                    // B9
+        if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
         f32x16 dE = rn_zero16();
 #pragma unroll
         for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
+        __syncthreads();                                                    // B10
 
-        // ---- weight gradients through the wave-private staging image
-        //      rows 0..31: dY tile, rows 32..63: X tile
-        const int16_t* map = a.dwmap;
-        // Wr3: dY = dO (rows 0..15; 16..31 zero), X = R2
-        rn_stage_frag(stg, 0, 0, dO); rn_stage_frag(stg, 0, 1, z8);
-#pragma unroll
-        for (int nn = 0; nn < 2; ++nn) {
-            rn_stage_frag(stg, 32, 0, st.r2[2 * nn]); rn_stage_frag(stg, 32, 1, st.r2[2 * nn + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + (0 + nn) * 1024, sDW, ginv);
-            wave_lds_fence();
-        }
-        // Wr2: dY = dR2, X = R1
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            rn_stage_frag(stg, 0, 0, dr2f[2 * m]); rn_stage_frag(stg, 0, 1, dr2f[2 * m + 1]);
-#pragma unroll
-            for (int nn = 0; nn < 2; ++nn) {
-                rn_stage_frag(stg, 32, 0, st.r1[2 * nn]);
-                rn_stage_frag(stg, 32, 1, st.r1[2 * nn + 1]);
-                wave_lds_fence();
-                rn_dw_tile(stg, 0, stg, 32, map + (2 + 2 * m + nn) * 1024, sDW, ginv);
-                wave_lds_fence();
-            }
-        }
-        // Wr1: dY = dR1, X = [SH | geo 1..16]
-        rn_stage_frag(stg, 32, 0, st.sh); rn_stage_frag(stg, 32, 1, st.gin);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            rn_stage_frag(stg, 0, 0, dr1f[2 * m]); rn_stage_frag(stg, 0, 1, dr1f[2 * m + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + (6 + m) * 1024, sDW, ginv);
-            wave_lds_fence();
-        }
-        // Wg2: dY = dG, X = H1
-        rn_stage_frag(stg, 0, 0, dg0); rn_stage_frag(stg, 0, 1, dg1);
-#pragma unroll
-        for (int nn = 0; nn < 2; ++nn) {
-            rn_stage_frag(stg, 32, 0, st.h1[2 * nn]); rn_stage_frag(stg, 32, 1, st.h1[2 * nn + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + (8 + nn) * 1024, sDW, ginv);
-            wave_lds_fence();
-        }
-        // Wg1: dY = dH1, X = E
-        rn_stage_frag(stg, 32, 0, st.e0); rn_stage_frag(stg, 32, 1, st.e1);
-#pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            rn_stage_frag(stg, 0, 0, dh1f[2 * m]); rn_stage_frag(stg, 0, 1, dh1f[2 * m + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + (10 + m) * 1024, sDW, ginv);
-            wave_lds_fence();
-        }
-
-        // ---- hash-grid gradient scatter.  Stage dE [32 samples][32 feat] f32
-        //      and the unit coords, then 4 samples x 8 corners x 2 features per
-        //      wave instruction, level by level.
-        float* sdE = reinterpret_cast<float*>(stg);         // 32 x 33 floats
+        // ---- hash-grid gradient scatter from the wave's own image region:
+        //      dE [32 samples][32 features] f32 + unit coords.  lane = (level
+        //      within a group of 4, corner, feature); each lane walks the
+        //      tile's samples in ray order and merges runs of equal corner
+        //      index in a register: one atomic per run instead of per sample.
+        const float ginv = 1.0f / gscale;
+        float* sdE = reinterpret_cast<float*>(imgY);        // 32 x 33 floats
         float* sU = sdE + 32 * 33;                          // 32 x 4 floats
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int row = (i & 3) + 8 * (i >> 2) + 4 * h;  // feature
             sdE[c * 33 + row] = valid ? dE[i] * ginv : 0.f;
         }
-        if (h == 0) { sU[c * 4 + 0] = ux; sU[c * 4 + 1] = uy; sU[c * 4 + 2] = uz; sU[c * 4 + 3] = valid ? 1.f : 0.f; }
-        wave_lds_fence();
-        const int sg = lane >> 4, corner = (lane >> 1) & 7, feat = lane & 1;
-        const int64_t tile_base = tile * 32;
+        if (h == 0) { sU[c * 4 + 0] = ux; sU[c * 4 + 1] = uy; sU[c * 4 + 2] = uz; }
+        rn_lds_order();
+        if (a.dbg & 4) continue;
+        const int lq = lane >> 4, corner = (lane >> 1) & 7, feat = lane & 1;
+        const int64_t rem = n - tile * 32;
+        const int nv = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
 #pragma unroll 1
-        for (int l = 0; l < RN_L; ++l) {
-            const float sc = a.gm.scale[l];
-            const uint32_t lvl_off = a.gm.offset[l];
+        for (int grp = 0; grp < 4; ++grp) {
+            const int l = 4 * grp + lq;
+            const float sc = sT.sc[l];
+            const uint32_t lvl_off = sT.off[l];
+            uint32_t cur = 0xffffffffu;
+            float acc = 0.f;
 #pragma unroll 2
-            for (int gi = 0; gi < 8; ++gi) {
-                const int smp = 4 * gi + sg;
-                if (tile_base + smp >= n) continue;
+            for (int smp = 0; smp < nv; ++smp) {
                 const float vx = sU[smp * 4], vy = sU[smp * 4 + 1], vz = sU[smp * 4 + 2];
                 const LevelPos p = level_pos(sc, vx, vy, vz);
-                const uint32_t idx = grid_index(a.gm, l, p.gx + (corner & 1),
+                const uint32_t idx = grid_index(sT, a.gm, l, p.gx + (corner & 1),
                                                 p.gy + ((corner >> 1) & 1),
                                                 p.gz + ((corner >> 2) & 1));
                 const float g = corner_weight(p, corner) * sdE[smp * 33 + 2 * l + feat];
-                atomicAdd(&a.grid_grad[2 * (size_t)(lvl_off + idx) + feat], g);
+                if (idx == cur) {
+                    acc += g;
+                } else {
+                    if (cur != 0xffffffffu) {
+                        if (a.dbg & 1) asm volatile("" :: "v"(acc), "v"(cur));
+                        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                                acc, grad_rs, (int)(8u * (lvl_off + cur) + 4u * feat), 0, 0);
+                    }
+                    cur = idx;
+                    acc = g;
+                }
+            }
+            if (cur != 0xffffffffu) {
+                if (a.dbg & 1) asm volatile("" :: "v"(acc), "v"(cur));
+                else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                        acc, grad_rs, (int)(8u * (lvl_off + cur) + 4u * feat), 0, 0);
             }
         }
-        wave_lds_fence();
     }
-    __syncthreads();
-    float* dw = a.dw + (size_t)k * FIELD_PARAMS;
-    for (int i = threadIdx.x; i < FIELD_PARAMS; i += blockDim.x) {
-        const float v = sDW[i];
-        if (v != 0.f) atomicAdd(&dw[i], v);
+    // ---- flush the owned dW tiles
+    if (cur_scale != 0.f && do_dw) {
+        float* dw = a.dw + (size_t)k * FIELD_PARAMS;
+        const float inv = 1.0f / cur_scale;
+        if (wid < 2) {
+            dw_flush<DW_ROWS_LT3>(accA, dw, 9280, 64, 0, 32 * wid, inv);   // rgb3
+            dw_flush<DW_GEO>(accB, dw, 2048, 64, 0, 32 * wid, inv);        // geo2
+        } else if (wid < 6) {
+            const int mm = (wid - 2) >> 1, nn = (wid - 2) & 1;
+            dw_flush<DW_PLAIN>(accA, dw, 5184, 64, 32 * mm, 32 * nn, inv); // rgb2
+            if (wid < 4) dw_flush<DW_PLAIN>(accB, dw, 0, 32, 32 * (wid - 2), 0, inv);  // geo1
+        } else {
+            dw_flush<DW_PLAIN>(accA, dw, 3136, 32, 32 * (wid - 6), 0, inv); // rgb1
+        }
     }
 }
 
@@ -503,11 +622,14 @@ int fill_args(FieldArgs& a, const float* xyz_min, const float* extent, const uin
               const uint32_t* hsize, const uint32_t* res, const float* scale) {
     for (int d = 0; d < 3; ++d) { a.xyz_min[d] = xyz_min[d]; a.extent[d] = extent[d]; }
     a.gm.dense_mask = 0;
+    a.gm.pow2_mask = 0;
+    a.grid_bytes = 4u * (offsets[RN_L - 1] + hsize[RN_L - 1]);
     for (int l = 0; l < RN_L; ++l) {
         a.gm.offset[l] = offsets[l]; a.gm.hsize[l] = hsize[l]; a.gm.res[l] = res[l];
         a.gm.scale[l] = scale[l];
         const uint64_t r = res[l];
         if (r * r * r <= (uint64_t)hsize[l]) a.gm.dense_mask |= 1u << l;
+        if (hsize[l] && (hsize[l] & (hsize[l] - 1u)) == 0) a.gm.pow2_mask |= 1u << l;
     }
     return 0;
 }
@@ -515,6 +637,8 @@ int fill_args(FieldArgs& a, const float* xyz_min, const float* extent, const uin
 }  // namespace
 
 extern "C" {
+
+void rn_set_debug_flags(int flags) { g_field_dbg = flags; }
 
 int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,
                 int32_t n_models, int64_t dst_stride, void* dst, void* stream) {
@@ -583,6 +707,7 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
+    a.dbg = g_field_dbg;
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags; a.dwmap = dw_map;
     a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
     dim3 grid(blocks_per_model, n_models);

@@ -105,6 +105,7 @@ k_gate_fwd(GateArgs a) {
     const int64_t n_tiles = (a.n_rays + 31) / 32;
     for (int64_t tile = (int64_t)blockIdx.x * GATE_WAVES + threadIdx.x / RN_WAVE; tile < n_tiles;
          tile += (int64_t)gridDim.x * GATE_WAVES) {
+        rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
         const int64_t r = tile * 32 + c;
         const bool valid = r < a.n_rays;
         GateState st;
@@ -128,28 +129,53 @@ k_gate_fwd(GateArgs a) {
     }
 }
 
-__device__ __forceinline__ void wave_lds_fence() {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+
+// gate output layer dW: rows < K of dz x H3 (W4 at 12672, 64 inputs)
+__device__ __forceinline__ void rn_dw_tile_gate_out(const rn_half* img_y, int ya, const rn_half* img_x,
+                                                    int xa, float* dw_lds, int K, float inv_scale) {
+    f32x16 acc = rn_zero16();
+    acc = rn_mfma(rn_img_read(img_y, ya, 0), rn_img_read(img_x, xa, 0), acc);
+    acc = rn_mfma(rn_img_read(img_y, ya, 1), rn_img_read(img_x, xa, 1), acc);
+    const int lane = rn_lane(), col = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (row < K) atomicAdd(dw_lds + 12672 + row * 64 + xa + col, acc[i] * inv_scale);
+    }
 }
 
-#define GSTG_HALFS (64 * RN_STG_STRIDE)
+// gate input layer dW: dH0 rows x 6 inputs (W0 at 0, [64][6])
+__device__ __forceinline__ void rn_dw_tile_gate_in(const rn_half* img_y, int ya, const rn_half* img_x,
+                                                   float* dw_lds, int out_base, float inv_scale) {
+    f32x16 acc = rn_zero16();
+    acc = rn_mfma(rn_img_read(img_y, ya, 0), rn_img_read(img_x, 0, 0), acc);
+    acc = rn_mfma(rn_img_read(img_y, ya, 1), rn_img_read(img_x, 0, 1), acc);
+    const int lane = rn_lane(), col = lane & 31, h = lane >> 5;
+    if (col >= 6) return;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        atomicAdd(dw_lds + (out_base + row) * 6 + col, acc[i] * inv_scale);
+    }
+}
 
 __global__ void __launch_bounds__(GATE_WAVES * 64)
 k_gate_bwd(GateArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[GATE_FRAGS * RN_FRAG_HALFS];
-    __shared__ __attribute__((aligned(16))) rn_half sStg[GATE_WAVES * GSTG_HALFS];
+    __shared__ __attribute__((aligned(16))) rn_half sImg[GATE_WAVES * 2 * RN_IMG_HALFS];
     __shared__ __attribute__((aligned(16))) float sDW[GATE_MAX_PARAMS];
     rn_block_copy16(sW, a.frags, GATE_FRAGS * RN_FRAG_BYTES);
     for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) sDW[i] = 0.f;
     __syncthreads();
     const int wid = threadIdx.x / RN_WAVE;
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
-    rn_half* stg = sStg + wid * GSTG_HALFS;
+    rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
+    rn_half* imgX = imgY + RN_IMG_HALFS;
     const half8 z8 = rn_zero8();
     const int64_t n_tiles = (a.n_rays + 31) / 32;
     for (int64_t tile = (int64_t)blockIdx.x * GATE_WAVES + wid; tile < n_tiles;
          tile += (int64_t)gridDim.x * GATE_WAVES) {
+        rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
         const int64_t r = tile * 32 + c;
         const bool valid = r < a.n_rays;
         GateState st;
@@ -197,41 +223,39 @@ k_gate_bwd(GateArgs a) {
             rn_acc_to_frags_masked(b0, st.h[L - 1][0], st.h[L - 1][1], dh[L - 1][0], dh[L - 1][1]);
             rn_acc_to_frags_masked(b1, st.h[L - 1][2], st.h[L - 1][3], dh[L - 1][2], dh[L - 1][3]);
         }
-        const int16_t* map = a.dwmap;
-        // W4: dY = dz (rows 0..15), X = H3
-        rn_stage_frag(stg, 0, 0, dz0); rn_stage_frag(stg, 0, 1, z8);
+        // W4: dY = dz (features 0..15, 16..31 zero), X = H3
+        rn_img_write(imgY, 0, dz0); rn_img_write(imgY, 1, z8);
 #pragma unroll
-        for (int nn = 0; nn < 2; ++nn) {
-            rn_stage_frag(stg, 32, 0, st.h[3][2 * nn]); rn_stage_frag(stg, 32, 1, st.h[3][2 * nn + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + (14 + nn) * 1024, sDW, ginv);
-            wave_lds_fence();
-        }
+        for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h[3][q]);
+        rn_lds_order();
+        rn_dw_tile_gate_out(imgY, 0, imgX, 0, sDW, a.K, ginv);
+        rn_dw_tile_gate_out(imgY, 0, imgX, 32, sDW, a.K, ginv);
+        rn_lds_order();
         // W1..W3: dY = dH_L, X = H_{L-1}
 #pragma unroll
         for (int L = 1; L <= 3; ++L) {
 #pragma unroll
-            for (int m = 0; m < 2; ++m) {
-                rn_stage_frag(stg, 0, 0, dh[L][2 * m]); rn_stage_frag(stg, 0, 1, dh[L][2 * m + 1]);
-#pragma unroll
-                for (int nn = 0; nn < 2; ++nn) {
-                    rn_stage_frag(stg, 32, 0, st.h[L - 1][2 * nn]);
-                    rn_stage_frag(stg, 32, 1, st.h[L - 1][2 * nn + 1]);
-                    wave_lds_fence();
-                    rn_dw_tile(stg, 0, stg, 32, map + (2 + 4 * (L - 1) + 2 * m + nn) * 1024, sDW, ginv);
-                    wave_lds_fence();
-                }
+            for (int q = 0; q < 4; ++q) {
+                rn_img_write(imgY, q, dh[L][q]);
+                rn_img_write(imgX, q, st.h[L - 1][q]);
             }
-        }
-        // W0: dY = dH0, X = input (rows 0..15; 16..31 zero)
-        rn_stage_frag(stg, 32, 0, st.x); rn_stage_frag(stg, 32, 1, z8);
+            rn_lds_order();
 #pragma unroll
-        for (int m = 0; m < 2; ++m) {
-            rn_stage_frag(stg, 0, 0, dh[0][2 * m]); rn_stage_frag(stg, 0, 1, dh[0][2 * m + 1]);
-            wave_lds_fence();
-            rn_dw_tile(stg, 0, stg, 32, map + m * 1024, sDW, ginv);
-            wave_lds_fence();
+            for (int m = 0; m < 2; ++m)
+#pragma unroll
+                for (int nn = 0; nn < 2; ++nn)
+                    rn_dw_tile<DW_PLAIN>(imgY, 32 * m, imgX, 32 * nn, sDW, 384 + 4096 * (L - 1),
+                                         64, 32 * m, 32 * nn, ginv);
+            rn_lds_order();
         }
+        // W0: dY = dH0, X = input (features 0..15; 16..31 zero)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dh[0][q]);
+        rn_img_write(imgX, 0, st.x); rn_img_write(imgX, 1, z8);
+        rn_lds_order();
+        rn_dw_tile_gate_in(imgY, 0, imgX, sDW, 0, ginv);
+        rn_dw_tile_gate_in(imgY, 32, imgX, sDW, 32, ginv);
+        rn_lds_order();
     }
     __syncthreads();
     for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) {

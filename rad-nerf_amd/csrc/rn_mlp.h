@@ -77,42 +77,83 @@ __device__ __forceinline__ void rn_block_copy16(void* lds, const void* g, int n_
 }
 
 // ---------------------------------------------------------------------------
-// dW staging: an activation fragment (B-operand form, k-step q of a tile
-// whose rows start at row0) is written into a wave-private LDS image
-// [row][32 samples] (f16, row stride RN_STG_STRIDE halfs) so that the
-// samples become the contraction index of the weight-gradient MFMA.
+// dW staging.  The weight gradient dW = dY . X^T contracts over the samples,
+// which live on the lanes of the accumulator layout, so (dY, X) go through a
+// wave-private LDS image in SAMPLE-major order img[sample][feature] (row
+// stride RN_IMG_STRIDE halfs): each lane stores its fragment with two 8-byte
+// ds_write_b64 (4 consecutive features each), and the MFMA operands
+// [feature][8 consecutive samples] come back with two ds_read_b64_tr_b16
+// (gfx950 transposed read, cdna_hip_programming.md §5.5 T10).
+// Row stride 68 halfs: conflict-free b64 writes (16 rows -> 16 bank pairs).
 // ---------------------------------------------------------------------------
-#define RN_STG_STRIDE 40   // 32 samples + 8 pad halfs (80 B rows)
+#define RN_IMG_STRIDE 68
+#define RN_IMG_HALFS (32 * RN_IMG_STRIDE)
 
-__device__ __forceinline__ void rn_stage_frag(rn_half* stg, int row0, int q, const half8& f) {
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef short rn_s4 __attribute__((__vector_size__(4 * sizeof(short))));
+typedef __attribute__((address_space(3))) rn_s4 rn_lds_s4;
+
+// fragment q (B-operand form, k-step q of a multi-tile activation) -> image
+__device__ __forceinline__ void rn_img_write(rn_half* img, int q, const half8& f) {
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    const int f0 = 32 * (q >> 1) + 16 * (q & 1) + 4 * h;
+    half4 lo, hi;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        const int row = row0 + 16 * (q & 1) + 8 * (j >> 2) + 4 * h + (j & 3) + 32 * (q >> 1);
-        stg[row * RN_STG_STRIDE + c] = f[j];
-    }
+    for (int j = 0; j < 4; ++j) { lo[j] = f[j]; hi[j] = f[4 + j]; }
+    *reinterpret_cast<half4*>(img + c * RN_IMG_STRIDE + f0) = lo;
+    *reinterpret_cast<half4*>(img + c * RN_IMG_STRIDE + f0 + 8) = hi;
 }
 
-// operand fragment for the dW MFMA: rows (row_base + lane&31), samples 16s+8h..+7
-__device__ __forceinline__ half8 rn_stage_read(const rn_half* stg, int row_base, int s) {
-    const int lane = rn_lane(), r = lane & 31, h = lane >> 5;
-    return *reinterpret_cast<const half8*>(stg + (row_base + r) * RN_STG_STRIDE + 16 * s + 8 * h);
+__device__ __forceinline__ half4 rn_tr_read(const rn_half* p) {
+    rn_s4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((rn_lds_s4*)(p));
+    return __builtin_bit_cast(half4, v);
 }
 
-// dW tile (rows of dY image at ya, rows of X image at xa) over the 32 samples
-// of the staged tile, accumulated into the block's LDS fp32 gradient through
-// the (tile, reg, lane) -> parameter map.  map < 0 = padding.
-__device__ __forceinline__ void rn_dw_tile(const rn_half* stg_y, int ya, const rn_half* stg_x,
-                                           int xa, const int16_t* __restrict__ map,
-                                           float* dw_lds, float inv_scale) {
+// dW MFMA operand: features fbase + (lane&31), samples 16s + 8h + 0..7
+__device__ __forceinline__ half8 rn_img_read(const rn_half* img, int fbase, int s) {
+    const int l = rn_lane(), g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+    const int col = fbase + 16 * (g & 1) + 4 * p;
+    const int sb = 16 * s + 8 * (g >> 1);
+    const half4 a = rn_tr_read(img + (sb + q) * RN_IMG_STRIDE + col);
+    const half4 b = rn_tr_read(img + (sb + 4 + q) * RN_IMG_STRIDE + col);
+    half8 r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) { r[j] = a[j]; r[4 + j] = b[j]; }
+    return r;
+}
+
+// compiler-only ordering point between LDS image writes and reads of one
+// wave (a wave's LDS operations execute in order; nothing to wait for)
+__device__ __forceinline__ void rn_lds_order() { asm volatile("" ::: "memory"); }
+
+// dW tile: dY features [ya, ya+32) x X features [xa, xa+32) over the 32
+// samples of the staged tile, accumulated (x inv_scale) into the block's LDS
+// fp32 gradient (row-major [out][in] master layout at `off`, `ncols` inputs).
+// Output row i of the tile is dY feature ya+i -> weight row out_base + i
+// (DW_PLAIN), only rows < 3 exist (DW_ROWS_LT3: rgb output layer), or the
+// geo-net remap rows 0..15 -> outputs 1..16, row 16 -> output 0 (DW_GEO).
+#define DW_PLAIN 0
+#define DW_ROWS_LT3 1
+#define DW_GEO 2
+template <int MODE>
+__device__ __forceinline__ void rn_dw_tile(const rn_half* img_y, int ya, const rn_half* img_x,
+                                           int xa, float* dw_lds, int off, int ncols,
+                                           int out_base, int in_base, float inv_scale,
+                                           int dbg = 0) {
     f32x16 acc = rn_zero16();
-    acc = rn_mfma(rn_stage_read(stg_y, ya, 0), rn_stage_read(stg_x, xa, 0), acc);
-    acc = rn_mfma(rn_stage_read(stg_y, ya, 1), rn_stage_read(stg_x, xa, 1), acc);
-    const int lane = rn_lane();
+    acc = rn_mfma(rn_img_read(img_y, ya, 0), rn_img_read(img_x, xa, 0), acc);
+    acc = rn_mfma(rn_img_read(img_y, ya, 1), rn_img_read(img_x, xa, 1), acc);
+    if (dbg & 8) { asm volatile("" :: "v"(acc)); return; }
+    const int lane = rn_lane(), col = lane & 31, h = lane >> 5;
+    float* base = dw_lds + off + in_base + col;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-        const int p = map[i * 64 + lane];
-        if (p >= 0) atomicAdd(&dw_lds[p], acc[i] * inv_scale);
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+        int out;
+        if (MODE == DW_PLAIN) out = out_base + row;
+        else if (MODE == DW_ROWS_LT3) out = row < 3 ? row : -1;
+        else out = row < 16 ? row + 1 : (row == 16 ? 0 : -1);
+        if (out >= 0) atomicAdd(base + out * ncols, acc[i] * inv_scale);
     }
 }
 

@@ -77,6 +77,9 @@ class _Lib:
         self.handle.rn_last_error.restype = ctypes.c_char_p
         self.handle.rn_last_error.argtypes = []
         self.handle.rn_version.restype = ctypes.c_int
+        self.handle.rn_set_debug_flags.argtypes = [ctypes.c_int]
+        self.handle.rn_set_debug_flags.restype = None
+        self.set_debug_flags = self.handle.rn_set_debug_flags
         self.path = path
         for name in SIGNATURES:
             setattr(self, name[3:], _Checked(self.handle, name))
@@ -94,4 +97,4 @@ def lib():
 
 
 def exported_symbols():
-    return ["rn_version", "rn_last_error"] + list(SIGNATURES)
+    return ["rn_version", "rn_last_error", "rn_set_debug_flags"] + list(SIGNATURES)
