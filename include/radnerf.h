@@ -126,7 +126,9 @@ int rn_ml_composite_bw(const float* dL_drgb, const float* dL_dopacity, const flo
  * Sample input: xyzs/dirs (n_samples, 3) [single model], or, when xyzs is
  * NULL, compact (ts, ray_of) + rays with per-model seg_base/seg_count.
  * level_* (16 entries) and xyz_min/extent (3) are HOST arrays read at launch;
- * frags = packed f16 weights (device), dw_map = layout.field_dw_map().      */
+ * frags = packed f16 weights (device).
+ * rn_field_bwd ADDS into grid_grad (fp32, tcnn layout) and dw (fp32, K x
+ * FIELD_PARAMS); the caller zeroes them when a fresh gradient is wanted.    */
 int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
                  const int32_t* ray_of, const float* rays_o, const float* rays_d,
                  const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
@@ -139,8 +141,8 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
-                 const float* extent, const void* frags, const int16_t* dw_map,
-                 const float* dL_dsigma, const float* dL_drgb, float* grid_grad, float* dw,
+                 const float* extent, const void* frags, const float* dL_dsigma,
+                 const float* dL_drgb, float* grid_grad, float* dw,
                  int32_t blocks_per_model, void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------

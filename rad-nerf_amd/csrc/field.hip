@@ -49,7 +49,6 @@ struct FieldArgs {
     const rn_half* grid;      // [entries][2] f16
     float* grid_grad;         // [entries][2] f32
     const rn_half* frags;     // [K][FIELD_FRAGS][512]
-    const int16_t* dwmap;     // [FIELD_DW_TILES][16][64]
     float* dw;                // [K][FIELD_PARAMS]
     float* sigma; float* rgb; // forward outputs
     const float* dsigma; const float* drgb;               // backward seeds
@@ -110,19 +109,28 @@ __device__ __forceinline__ void lv_stage(LvTab& t, const GridMeta& gm) {
     }
 }
 
-// tcnn grid_index (Linear, coherent prime hash); masks are wave-uniform SGPRs
-__device__ __forceinline__ uint32_t grid_index(const LvTab& T, const GridMeta& gm, int l,
-                                               uint32_t x, uint32_t y, uint32_t z) {
-    uint32_t idx;
-    if ((gm.dense_mask >> l) & 1u) {
-        const uint32_t r = T.res[l];
-        idx = x + y * r + z * r * r;
-    } else {
-        idx = x ^ (y * 2654435761u) ^ (z * 805459861u);
-    }
-    const uint32_t hs = T.hs[l];
-    if ((gm.pow2_mask >> l) & 1u) return idx & (hs - 1u);   // hashed levels: T = 2^k
-    return idx < hs ? idx : idx % hs;
+// Per-lane constants of one level, hoisted out of sample loops.
+struct LvConst {
+    uint32_t off, hs, res, res2;
+    float sc;
+    bool dense;
+};
+
+__device__ __forceinline__ LvConst lv_const(const LvTab& T, const GridMeta& gm, int l) {
+    LvConst c;
+    c.off = T.off[l]; c.hs = T.hs[l]; c.res = T.res[l]; c.res2 = c.res * c.res; c.sc = T.sc[l];
+    c.dense = (gm.dense_mask >> l) & 1u;
+    return c;
+}
+
+// tcnn grid_index (Linear, coherent prime hash), branch-free.  Dense levels:
+// index < res^3 + res^2 + res < 2*hsize, so `% hsize` is one conditional
+// subtract; hashed levels have hsize = 2^log2_T, so it is a mask.
+__device__ __forceinline__ uint32_t grid_index(const LvConst& c, uint32_t x, uint32_t y, uint32_t z) {
+    const uint32_t di = x + y * c.res + z * c.res2;
+    const uint32_t hi = x ^ (y * 2654435761u) ^ (z * 805459861u);
+    const uint32_t dm = di >= c.hs ? di - c.hs : di;
+    return c.dense ? dm : (hi & (c.hs - 1u));
 }
 
 struct LevelPos { uint32_t gx, gy, gz; float fx, fy, fz; };
@@ -142,6 +150,10 @@ __device__ __forceinline__ float corner_weight(const LevelPos& p, int c) {
     w *= (c & 2) ? p.fy : 1.0f - p.fy;
     w *= (c & 4) ? p.fz : 1.0f - p.fz;
     return w;
+}
+
+__device__ __forceinline__ uint32_t corner_index(const LvConst& c, const LevelPos& p, int corner) {
+    return grid_index(c, p.gx + (corner & 1), p.gy + ((corner >> 1) & 1), p.gz + ((corner >> 2) & 1));
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rn_rsrc(const void* p, uint32_t bytes) {
@@ -164,14 +176,12 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
         uint32_t off[16];
 #pragma unroll
         for (int u = 0; u < 2; ++u) {
-            const int l = lane_level(qb + u, h);
-            P[u] = level_pos(T.sc[l], ux, uy, uz);
-            const uint32_t lo = T.off[l];
+            const LvConst lc = lv_const(T, a.gm, lane_level(qb + u, h));
+            P[u] = level_pos(lc.sc, ux, uy, uz);
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const uint32_t idx = grid_index(T, a.gm, l, P[u].gx + (c & 1),
-                                                P[u].gy + ((c >> 1) & 1), P[u].gz + ((c >> 2) & 1));
-                off[8 * u + c] = valid ? 4u * (lo + idx) : RN_OOB;
+                const uint32_t idx = corner_index(lc, P[u], c);
+                off[8 * u + c] = valid ? 4u * (lc.off + idx) : RN_OOB;
             }
         }
         uint32_t raw[16];
@@ -346,6 +356,77 @@ k_field_fwd(FieldArgs a) {
 // ---------------------------------------------------------------------------
 #define BWD_WAVES 8
 
+// ---------------------------------------------------------------------------
+// Hash-grid gradient scatter of one block iteration (256 ray-ordered samples).
+//
+// Global float atomics on gfx950 execute at the memory side; their cost is one
+// 64-B request per distinct 64-B segment a wave instruction touches
+// (MI355X_MICROARCH.md "Global float atomics"; measured here: halving the
+// active lanes or making every target L2-resident leaves the kernel time
+// unchanged, dropping the four finest levels' atomics halves it).  So the
+// scatter is designed to issue as few distinct (instruction, segment) pairs
+// as possible:
+//
+//  * wave w owns levels w and 15-w (one coarse + one fine, for balance);
+//    lane = (half of the block's samples, level, corner, feature); each lane
+//    walks its 128 samples in ray order holding one accumulator for its
+//    corner of the current cell;
+//  * when the cell changes by delta, the accumulator of old corner c is handed
+//    (one ds_bpermute) to the lane of new corner c - delta when that is still
+//    a corner of the new cell: an entry shared by consecutive cells is added
+//    to once per visit of the ray, not once per cell (tcnn adds it per sample);
+//    only corners that leave the cell are issued.  Requests/sample on the
+//    bench workload (tools/atomic_sim.py): 34.2 with per-corner run merging,
+//    27.2 with the hand-over.
+// ---------------------------------------------------------------------------
+#define SG_STRIDE 34
+
+__device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvTab& sT,
+                                                   const float* sG, const float* sU, int nblk,
+                                                   __amdgpu_buffer_rsrc_t grad_rs) {
+    const int lane = rn_lane();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+    const int half = lane >> 5, corner = (lane >> 1) & 7, feat = lane & 1;
+    const int cx = corner & 1, cy = (corner >> 1) & 1, cz = corner >> 2;
+    const int l = ((lane >> 4) & 1) ? (RN_L - 1 - wid) : wid;
+    const LvConst lc = lv_const(sT, a.gm, l);
+    const int n0 = min(nblk, BWD_WAVES * 16);             // samples of half 0 (the longer)
+    const int nh = half ? nblk - n0 : n0;
+    const int s_base = half * (BWD_WAVES * 16);
+    int gx = -1000, gy = 0, gz = 0;                       // current cell (none yet)
+    uint32_t cur = 0;
+    float acc = 0.f;
+    auto emit = [&](float v, uint32_t idx) {
+        if (a.dbg & 1) asm volatile("" :: "v"(v), "v"(idx));
+        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
+                 v, grad_rs, (int)(8u * (lc.off + idx) + 4u * feat), 0, 0);
+    };
+#pragma unroll 2
+    for (int j = 0; j < n0; ++j) {                        // wave-uniform trip count
+        const bool act = j < nh;
+        const int smp = s_base + (act ? j : 0);
+        const float* u = sU + smp * 4;
+        const LevelPos p = level_pos(lc.sc, u[0], u[1], u[2]);
+        const float g = corner_weight(p, corner) * sG[smp * SG_STRIDE + 2 * l + feat];
+        const int dx = (int)p.gx - gx, dy = (int)p.gy - gy, dz = (int)p.gz - gz;
+        // new corner c <- old corner c + delta (if that is a corner of the old cell)
+        const int ox = cx + dx, oy = cy + dy, oz = cz + dz;
+        const bool src_ok = (unsigned)ox <= 1u && (unsigned)oy <= 1u && (unsigned)oz <= 1u;
+        const int src = (lane & ~14) | ((src_ok ? ox + 2 * oy + 4 * oz : 0) << 1);
+        const float carried = __shfl(acc, src);
+        // old corner c survives as new corner c - delta
+        const int mx = cx - dx, my = cy - dy, mz = cz - dz;
+        const bool keep = (unsigned)mx <= 1u && (unsigned)my <= 1u && (unsigned)mz <= 1u;
+        if (act) {
+            if (!keep && gx != -1000) emit(acc, cur);
+            acc = (src_ok ? carried : 0.f) + g;
+            cur = corner_index(lc, p, corner);
+            gx = (int)p.gx; gy = (int)p.gy; gz = (int)p.gz;
+        }
+    }
+    if (gx != -1000) emit(acc, cur);
+}
+
 // dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
 __device__ __forceinline__ f32x16 dw_block_tile(const rn_half* sImg, int ya, int xa, f32x16 acc) {
 #pragma unroll
@@ -381,6 +462,10 @@ k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[BWD_WAVES];
     __shared__ LvTab sT;
+    // grid-gradient scatter staging: dL/dfeature rows and unit coordinates of
+    // the iteration's 256 samples
+    __shared__ __attribute__((aligned(16))) float sG[BWD_WAVES * 32 * SG_STRIDE];
+    __shared__ __attribute__((aligned(16))) float sU[BWD_WAVES * 32 * 4];
     const int k = blockIdx.y;
     rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                     FIELD_FRAGS * RN_FRAG_BYTES);
@@ -404,6 +489,8 @@ k_field_bwd(FieldArgs a) {
     //   w2: + g1(m=0)          w3: + g1(m=1)          w6, w7: r1(m)
     f32x16 accA = rn_zero16(), accB = rn_zero16();
     float cur_scale = 0.f;   // scale the accumulators are expressed at (0 = empty)
+
+    const bool do_sc = !(a.dbg & 4);
 
     for (int64_t it = blockIdx.x; it < n_iters; it += gridDim.x) {
         rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
@@ -528,57 +615,20 @@ k_field_bwd(FieldArgs a) {
         for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
         __syncthreads();                                                    // B10
 
-        // ---- hash-grid gradient scatter from the wave's own image region:
-        //      dE [32 samples][32 features] f32 + unit coords.  lane = (level
-        //      within a group of 4, corner, feature); each lane walks the
-        //      tile's samples in ray order and merges runs of equal corner
-        //      index in a register: one atomic per run instead of per sample.
-        const float ginv = 1.0f / gscale;
-        float* sdE = reinterpret_cast<float*>(imgY);        // 32 x 33 floats
-        float* sU = sdE + 32 * 33;                          // 32 x 4 floats
+        // ---- hash-grid gradient scatter (grid_scatter_block)
+        if (do_sc) {
+            const float ginv = 1.0f / gscale;
+            const int srow = wid * 32 + c;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int row = (i & 3) + 8 * (i >> 2) + 4 * h;  // feature
-            sdE[c * 33 + row] = valid ? dE[i] * ginv : 0.f;
-        }
-        if (h == 0) { sU[c * 4 + 0] = ux; sU[c * 4 + 1] = uy; sU[c * 4 + 2] = uz; }
-        rn_lds_order();
-        if (a.dbg & 4) continue;
-        const int lq = lane >> 4, corner = (lane >> 1) & 7, feat = lane & 1;
-        const int64_t rem = n - tile * 32;
-        const int nv = rem <= 0 ? 0 : (rem < 32 ? (int)rem : 32);
-#pragma unroll 1
-        for (int grp = 0; grp < 4; ++grp) {
-            const int l = 4 * grp + lq;
-            const float sc = sT.sc[l];
-            const uint32_t lvl_off = sT.off[l];
-            uint32_t cur = 0xffffffffu;
-            float acc = 0.f;
-#pragma unroll 2
-            for (int smp = 0; smp < nv; ++smp) {
-                const float vx = sU[smp * 4], vy = sU[smp * 4 + 1], vz = sU[smp * 4 + 2];
-                const LevelPos p = level_pos(sc, vx, vy, vz);
-                const uint32_t idx = grid_index(sT, a.gm, l, p.gx + (corner & 1),
-                                                p.gy + ((corner >> 1) & 1),
-                                                p.gz + ((corner >> 2) & 1));
-                const float g = corner_weight(p, corner) * sdE[smp * 33 + 2 * l + feat];
-                if (idx == cur) {
-                    acc += g;
-                } else {
-                    if (cur != 0xffffffffu) {
-                        if (a.dbg & 1) asm volatile("" :: "v"(acc), "v"(cur));
-                        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                                acc, grad_rs, (int)(8u * (lvl_off + cur) + 4u * feat), 0, 0);
-                    }
-                    cur = idx;
-                    acc = g;
-                }
+            for (int i = 0; i < 16; ++i) {
+                const int f = (i & 3) + 8 * (i >> 2) + 4 * h;  // feature
+                sG[srow * SG_STRIDE + f] = dE[i] * ginv;
             }
-            if (cur != 0xffffffffu) {
-                if (a.dbg & 1) asm volatile("" :: "v"(acc), "v"(cur));
-                else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                        acc, grad_rs, (int)(8u * (lvl_off + cur) + 4u * feat), 0, 0);
-            }
+            if (h == 0) { sU[srow * 4 + 0] = ux; sU[srow * 4 + 1] = uy; sU[srow * 4 + 2] = uz; }
+            const int64_t rem = n - it * (BWD_WAVES * 32);
+            const int nblk = rem < BWD_WAVES * 32 ? (int)rem : BWD_WAVES * 32;
+            __syncthreads();
+            grid_scatter_block(a, sT, sG, sU, nblk, grad_rs);
         }
     }
     // ---- flush the owned dW tiles
@@ -698,17 +748,16 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
-                 const float* extent, const void* frags, const int16_t* dw_map,
-                 const float* dL_dsigma, const float* dL_drgb, float* grid_grad, float* dw,
+                 const float* extent, const void* frags, const float* dL_dsigma,
+                 const float* dL_drgb, float* grid_grad, float* dw,
                  int32_t blocks_per_model, void* stream) {
     RN_CHECK_ARG(n_models >= 1 && n_samples >= 0 && blocks_per_model >= 1, "bad sizes");
     RN_CHECK_ARG(grid_f16 && level_offset && level_hsize && level_res && level_scale && xyz_min &&
-                 extent && frags && dw_map && dL_dsigma && dL_drgb && grid_grad && dw,
-                 "null pointer");
+                 extent && frags && dL_dsigma && dL_drgb && grid_grad && dw, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.dbg = g_field_dbg;
-    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags; a.dwmap = dw_map;
+    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
     dim3 grid(blocks_per_model, n_models);
     if (xyzs) {

@@ -158,10 +158,8 @@ class FusedMLRenderer:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
                      self.fwd_blocks, st)
         else:
-            self._ev("field_bwd", L.field_bwd, *common, m.dw_map(rays_o.device).data_ptr(),
-                     w.dsigma.data_ptr(),
-                        w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(), self.bwd_blocks,
-                        st)
+            self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
+                     w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(), self.bwd_blocks, st)
 
     # ----------------------------------------------------------------- backward
     def backward(self, rays_o, rays_d, gate_in2, gate, bg, dL_drgb, dL_dopacity, dL_ddepth,

@@ -1,0 +1,70 @@
+"""CPU: ray-batch data parallelism over torch.distributed (gloo, world size 2).
+Same code path as the RCCL run of bench.py --gpus N (radnerf_amd/dist.py)."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from radnerf_amd import dist as rdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    try:
+        r, local, w = rdist.init(backend="gloo")
+        assert (r, w) == (rank, world)
+        # disjoint contiguous ray shards covering the global batch
+        lo, hi = rdist.shard_rays(1000, r, w)
+        # flat-buffer gradient all-reduce (mean)
+        params = [torch.zeros(5, 2), torch.zeros(3), torch.zeros(4, 4)]
+        ar = rdist.GradAllReduce(params, "cpu")
+        for i, v in enumerate(ar.views):
+            v.fill_(float(rank + 1) * (i + 1))
+        views = ar.reduce()
+        ok_mean = all(torch.allclose(v, torch.full_like(v, 1.5 * (i + 1)))
+                      for i, v in enumerate(views))
+        # density buffers synchronised from rank 0
+        m = torch.nn.Module()
+        m.register_buffer("density_bitfield_0", torch.full((8,), rank, dtype=torch.uint8))
+        m.register_buffer("other", torch.full((2,), rank))
+        rdist.broadcast_buffers(m)
+        ok_bcast = bool((m.density_bitfield_0 == 0).all()) and int(m.other[0]) == rank
+        q.put((rank, lo, hi, ok_mean, ok_bcast))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, "error", repr(e), False, False))
+
+
+def test_gloo_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0][1:3] == (0, 500) and res[1][1:3] == (500, 1000), res
+    assert all(r[3] for r in res), res
+    assert all(r[4] for r in res), res
+
+
+def test_single_process_noop():
+    ar = rdist.GradAllReduce([torch.ones(3)], "cpu")
+    ar.views[0].fill_(2.0)
+    assert torch.equal(ar.reduce()[0], torch.full((3,), 2.0))
+    assert rdist.shard_rays(10, 0, 1) == (0, 10)
+    assert rdist.shard_rays(10, 2, 3) == (8, 10)

@@ -46,15 +46,6 @@ def _oracle_field(m, x, d, ind, scale):
     return sig, rgb, gp, mp
 
 
-def test_level_table_matches_oracle():
-    for scale in (0.5, 16.0):
-        a, b = LY.grid_levels(scale), fo.grid_levels(scale)
-        assert a["n_entries"] == b["n_entries"]
-        for k in ("offset", "hsize", "res"):
-            assert np.array_equal(a[k].astype(np.int64), b[k])
-        assert np.array_equal(a["scale"], b["scale"])
-
-
 @pytest.mark.parametrize("scale", [0.5, 16.0])
 def test_field_forward(cuda, scale):
     m = _model(cuda, scale)

@@ -18,7 +18,7 @@ from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 
 
 def main():
-    flags = [int(f) for f in (sys.argv[1:] or ["0", "1", "2", "4", "6"])]
+    flags = sys.argv[1:] or ["0", "1", "2", "4", "6"]
     dev = torch.device("cuda")
     B, K = 8192, 2
     m = MNGP(0.5, size=K, seed=3).to(dev)
@@ -43,7 +43,7 @@ def main():
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(f)
+            L.set_debug_flags(int(f))
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             r._field(False, o, d, st, gg, mg)
