@@ -380,9 +380,61 @@ k_field_fwd(FieldArgs a) {
 //    27.2 with the hand-over.
 // ---------------------------------------------------------------------------
 #define SG_STRIDE 34
+#define SC_RING 128          // records per stream ring (power of two, >= 64 + 16)
+
+// Finished runs are not issued by the lane that holds them: each of the
+// wave's 4 streams (half, level) compacts its finished runs (ballot + mbcnt)
+// into its own LDS ring of (byte offset, value) records and issues an atomic
+// instruction when 64 are pending, every lane active.  One instruction then
+// covers ~4-80 consecutive samples of ONE level of one ray, so entries of the
+// same 64-B segment that leave the cell at different steps (a ray moving
+// along x) share one request: 21.6 requests/sample (tools/atomic_sim.py).
+struct ScatterRing {
+    uint2* ring;             // this wave's 4 x SC_RING records
+    uint32_t head[4];        // per stream, wave-uniform
+    uint32_t tail;           // per lane: the tail of this lane's stream
+};
+
+__device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
+                                           __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+    const int lane = rn_lane();
+    asm volatile("" ::: "memory");
+    if ((uint32_t)lane < cnt) {
+        const uint2 r = R.ring[s * SC_RING + ((R.head[s] + lane) & (SC_RING - 1))];
+        if (dbg & 1) asm volatile("" :: "v"(r.x), "v"(r.y));
+        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(r.y), grad_rs,
+                                                             (int)r.x, 0, 0);
+    }
+    asm volatile("" ::: "memory");
+    R.head[s] += cnt;
+}
+
+// append this step's finished runs (lanes with `emit`) to their stream rings;
+// no issue here (ring_drain runs every 4 steps: 63 pending + 4 x 16 <= 128)
+__device__ __forceinline__ void ring_push(ScatterRing& R, bool emit, uint64_t smask, uint32_t off,
+                                          float v) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(emit) & smask;
+    const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
+    const int s = rn_lane() >> 4;
+    if (emit)
+        R.ring[s * SC_RING + ((R.tail + rank) & (SC_RING - 1))] = make_uint2(off, __float_as_uint(v));
+    R.tail += (uint32_t)(__builtin_popcount(lo) + __builtin_popcount(hi));
+}
+
+__device__ __forceinline__ void ring_drain(ScatterRing& R, uint32_t min_cnt,
+                                           __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t t = __builtin_amdgcn_readlane(R.tail, 16 * q);
+        const uint32_t pend = t - R.head[q];
+        if (pend >= min_cnt && pend > 0u) ring_issue(R, q, pend < 64u ? pend : 64u, grad_rs, dbg);
+    }
+}
 
 __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvTab& sT,
                                                    const float* sG, const float* sU, int nblk,
+                                                   ScatterRing& R,
                                                    __amdgpu_buffer_rsrc_t grad_rs) {
     const int lane = rn_lane();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
@@ -390,41 +442,49 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
     const int cx = corner & 1, cy = (corner >> 1) & 1, cz = corner >> 2;
     const int l = ((lane >> 4) & 1) ? (RN_L - 1 - wid) : wid;
     const LvConst lc = lv_const(sT, a.gm, l);
+    const uint64_t smask = 0xffffull << (16 * (lane >> 4));
     const int n0 = min(nblk, BWD_WAVES * 16);             // samples of half 0 (the longer)
     const int nh = half ? nblk - n0 : n0;
     const int s_base = half * (BWD_WAVES * 16);
+    const float* gcol = sG + 2 * l + feat;
     int gx = -1000, gy = 0, gz = 0;                       // current cell (none yet)
     uint32_t cur = 0;
     float acc = 0.f;
-    auto emit = [&](float v, uint32_t idx) {
-        if (a.dbg & 1) asm volatile("" :: "v"(v), "v"(idx));
-        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(
-                 v, grad_rs, (int)(8u * (lc.off + idx) + 4u * feat), 0, 0);
-    };
-#pragma unroll 2
-    for (int j = 0; j < n0; ++j) {                        // wave-uniform trip count
-        const bool act = j < nh;
-        const int smp = s_base + (act ? j : 0);
-        const float* u = sU + smp * 4;
-        const LevelPos p = level_pos(lc.sc, u[0], u[1], u[2]);
-        const float g = corner_weight(p, corner) * sG[smp * SG_STRIDE + 2 * l + feat];
-        const int dx = (int)p.gx - gx, dy = (int)p.gy - gy, dz = (int)p.gz - gz;
-        // new corner c <- old corner c + delta (if that is a corner of the old cell)
-        const int ox = cx + dx, oy = cy + dy, oz = cz + dz;
-        const bool src_ok = (unsigned)ox <= 1u && (unsigned)oy <= 1u && (unsigned)oz <= 1u;
-        const int src = (lane & ~14) | ((src_ok ? ox + 2 * oy + 4 * oz : 0) << 1);
-        const float carried = __shfl(acc, src);
-        // old corner c survives as new corner c - delta
-        const int mx = cx - dx, my = cy - dy, mz = cz - dz;
-        const bool keep = (unsigned)mx <= 1u && (unsigned)my <= 1u && (unsigned)mz <= 1u;
-        if (act) {
-            if (!keep && gx != -1000) emit(acc, cur);
-            acc = (src_ok ? carried : 0.f) + g;
-            cur = corner_index(lc, p, corner);
-            gx = (int)p.gx; gy = (int)p.gy; gz = (int)p.gz;
+    // software pipeline: this step's sample row is loaded one step ahead
+    float4 un = *reinterpret_cast<const float4*>(sU + s_base * 4);
+    float gn = gcol[s_base * SG_STRIDE];
+    for (int j0 = 0; j0 < n0; j0 += 4) {                  // wave-uniform trip count
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+            const int j = j0 + jj;
+            const bool act = j < nh;
+            const float4 uc = un;
+            const float gc = gn;
+            const int nx = s_base + (j + 1 < nh ? j + 1 : 0);
+            un = *reinterpret_cast<const float4*>(sU + nx * 4);
+            gn = gcol[nx * SG_STRIDE];
+            const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
+            const float g = corner_weight(p, corner) * gc;
+            const int dx = (int)p.gx - gx, dy = (int)p.gy - gy, dz = (int)p.gz - gz;
+            // new corner c <- old corner c + delta (if that is a corner of the old cell)
+            const int ox = cx + dx, oy = cy + dy, oz = cz + dz;
+            const bool src_ok = (unsigned)ox <= 1u && (unsigned)oy <= 1u && (unsigned)oz <= 1u;
+            const int src = (lane & ~14) | ((src_ok ? ox + 2 * oy + 4 * oz : 0) << 1);
+            const float carried = __shfl(acc, src);
+            // old corner c survives as new corner c - delta
+            const int mx = cx - dx, my = cy - dy, mz = cz - dz;
+            const bool keep = (unsigned)mx <= 1u && (unsigned)my <= 1u && (unsigned)mz <= 1u;
+            ring_push(R, act && !keep && gx != -1000, smask, 8u * (lc.off + cur) + 4u * feat, acc);
+            if (act) {
+                acc = (src_ok ? carried : 0.f) + g;
+                cur = corner_index(lc, p, corner);
+                gx = (int)p.gx; gy = (int)p.gy; gz = (int)p.gz;
+            }
         }
+        ring_drain(R, 64u, grad_rs, a.dbg);
     }
-    if (gx != -1000) emit(acc, cur);
+    ring_push(R, gx != -1000, smask, 8u * (lc.off + cur) + 4u * feat, acc);
+    ring_drain(R, 64u, grad_rs, a.dbg);
 }
 
 // dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
@@ -462,10 +522,7 @@ k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[BWD_WAVES];
     __shared__ LvTab sT;
-    // grid-gradient scatter staging: dL/dfeature rows and unit coordinates of
-    // the iteration's 256 samples
-    __shared__ __attribute__((aligned(16))) float sG[BWD_WAVES * 32 * SG_STRIDE];
-    __shared__ __attribute__((aligned(16))) float sU[BWD_WAVES * 32 * 4];
+    __shared__ uint2 sRing[BWD_WAVES * 4 * SC_RING];    // grid-gradient scatter rings
     const int k = blockIdx.y;
     rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                     FIELD_FRAGS * RN_FRAG_BYTES);
@@ -491,6 +548,17 @@ k_field_bwd(FieldArgs a) {
     float cur_scale = 0.f;   // scale the accumulators are expressed at (0 = empty)
 
     const bool do_sc = !(a.dbg & 4);
+    // scatter staging (dL/dfeature rows, unit coords of the iteration's 256
+    // samples) reuses the image region, free between B10 and the next B0
+    float* sG = reinterpret_cast<float*>(sImg);                        // [256][SG_STRIDE]
+    float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;                        // [256][4]
+    static_assert(BWD_WAVES * 32 * (SG_STRIDE + 4) * 4 <= BWD_WAVES * 2 * RN_IMG_HALFS * 2,
+                  "scatter staging must fit the image region");
+    ScatterRing R;
+    R.ring = sRing + wid * 4 * SC_RING;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) R.head[q] = 0;
+    R.tail = 0;
 
     for (int64_t it = blockIdx.x; it < n_iters; it += gridDim.x) {
         rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
@@ -628,9 +696,10 @@ k_field_bwd(FieldArgs a) {
             const int64_t rem = n - it * (BWD_WAVES * 32);
             const int nblk = rem < BWD_WAVES * 32 ? (int)rem : BWD_WAVES * 32;
             __syncthreads();
-            grid_scatter_block(a, sT, sG, sU, nblk, grad_rs);
+            grid_scatter_block(a, sT, sG, sU, nblk, R, grad_rs);
         }
     }
+    if (do_sc) ring_drain(R, 0u, grad_rs, a.dbg);
     // ---- flush the owned dW tiles
     if (cur_scale != 0.f && do_dw) {
         float* dw = a.dw + (size_t)k * FIELD_PARAMS;
