@@ -39,6 +39,11 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FIELD_BWD_BYTES_PER_SAMPLE = 16 + 24 + 1024
 # field forward: read 24 + hash gather 512 + sigma/rgb write 16
 FIELD_FWD_BYTES_PER_SAMPLE = 24 + 512 + 16
+# whole path fwd+bwd: 612 + 1112
+PATH_BYTES_PER_SAMPLE = 1724
+# MI355X_MICROARCH.md "Global float atomics": ~1.3 TB/s of added bytes at four
+# 64-B requests per 256-B wave instruction = 20.3 G requests/s chip-wide
+ATOMIC_PEAK_GREQ = 1.3e12 / 64 / 1e9
 
 
 def parse():
@@ -131,12 +136,14 @@ def main():
     samples_per_step_rank = int(samples_acc) / args.steps
     bwd_ms = kms.get("field_bwd", float("nan"))
     achieved = samples_per_step_rank * FIELD_BWD_BYTES_PER_SAMPLE / (bwd_ms * 1e-3) / 1e9
-    traffic = None
+    traffic, atom_req, pmc_samples = None, None, None
     if os.path.exists(args.traffic_json):
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             traffic = tj.get("field_bwd_bytes_per_launch")
+            atom_req = tj.get("field_bwd_atomic_requests")
+            pmc_samples = tj.get("samples_per_launch") or samples_per_step_rank
         except (OSError, ValueError):
             traffic = None
     roofline = {"kernel": "field_bwd", "bound": "hbm", "achieved": round(achieved, 1),
@@ -144,7 +151,19 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_sample": FIELD_BWD_BYTES_PER_SAMPLE,
                 "samples_per_launch": round(samples_per_step_rank),
-                "avg_launch_ms": round(bwd_ms, 4)}
+                "avg_launch_ms": round(bwd_ms, 4),
+                # the grid-gradient scatter is bound by the memory-side float-atomic
+                # request rate, not by HBM bytes (DESIGN.md "field_bwd")
+                "path_achieved_GBs": round(value / world * PATH_BYTES_PER_SAMPLE / 1e3, 1)}
+    if atom_req:
+        # requests per launch from the PMC pass (tools/pmc_traffic.py), scaled to
+        # this run's sample count; rate against the chip-wide atomic ceiling
+        req = atom_req * samples_per_step_rank / pmc_samples
+        rate = req / (bwd_ms * 1e-3) / 1e9
+        roofline["atomic"] = {"requests_per_launch": round(req), "requests_per_sample":
+                              round(req / samples_per_step_rank, 2),
+                              "achieved": round(rate, 2), "peak": ATOMIC_PEAK_GREQ, "unit": "G req/s",
+                              "frac": round(rate / ATOMIC_PEAK_GREQ, 3)}
 
     rgb_linf = None
     cpu_base = None

@@ -80,7 +80,8 @@ def test_fused_vs_dropin_vs_oracle(cuda, scale):
     e_op = np.abs(rf["opacity"].detach().cpu().numpy() - ores["opacity"]).max()
     e_de = np.abs(rf["depth"].detach().cpu().numpy() - ores["depth"]).max()
     print(f"scale {scale}: rgb Linf {e_rgb:.2e} opacity {e_op:.2e} depth {e_de:.2e}")
-    assert e_rgb <= 1e-3 and e_op <= 1e-3 and e_de <= 1e-3 * max(1, scale)
+    # north_star bar: rgb/depth/opacity within 1e-4 (fp32) of the reference path
+    assert e_rgb <= 1e-4 and e_op <= 1e-4 and e_de <= 1e-4 * max(1, scale)
     rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
     assert rel(gf[0].cpu().view(-1, 2).numpy(), ores["grid_grad"]) <= 5e-2
     assert rel(gf[1].cpu().numpy(), ores["mlp_grad"]) <= 5e-2

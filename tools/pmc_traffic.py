@@ -1,0 +1,66 @@
+"""Reduce rocprofv3 PMC passes to per-launch HBM traffic of the field kernels.
+
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> [<atomic_dir>] > traffic.json
+
+Each dir holds run_counter_collection.csv of one `rocprofv3 --pmc <counter>`
+pass over `bench.py` (separate passes: FETCH_SIZE and WRITE_SIZE cannot share
+one, MI355X_MICROARCH.md "rocprofv3 PMC slots").  Corrections as the guide
+prescribes for gfx950: FETCH_SIZE and WRITE_SIZE are in KiB; FETCH_SIZE counts
+64 B per 128-B request of a wide coalesced read, so it is doubled (our field
+kernels' reads are 4-16 B gathers, where the factor is uncalibrated: both the
+raw and the corrected figure are kept).  WRITE_SIZE counts float atomics
+exactly (one dword per lane).  TCC_EA0_ATOMIC (when collected) counts the 64-B
+atomic requests leaving L2.
+"""
+import csv
+import json
+import os
+import sys
+from collections import defaultdict
+
+KERNELS = {"field_bwd": "k_field_bwd", "field_fwd": "k_field_fwd"}
+
+
+def per_dispatch(d):
+    path = os.path.join(d, "run_counter_collection.csv")
+    vals = defaultdict(lambda: defaultdict(float))   # kernel -> dispatch -> value
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            name = row.get("Kernel_Name", "")
+            for key, pat in KERNELS.items():
+                if pat in name:
+                    vals[key][row["Dispatch_Id"]] += float(row["Counter_Value"])
+    return {k: sum(v.values()) / len(v) for k, v in vals.items() if v}
+
+
+def main():
+    fetch = per_dispatch(sys.argv[1])
+    write = per_dispatch(sys.argv[2])
+    atom = per_dispatch(sys.argv[3]) if len(sys.argv) > 3 and os.path.isdir(sys.argv[3]) else {}
+    samples = None
+    for d in sys.argv[1:3]:
+        try:
+            with open(d.rstrip("/") + ".log") as f:
+                for line in f:
+                    if line.startswith('{"metric"'):
+                        samples = json.loads(line)["config"]["samples_per_step_per_gpu"]
+        except (OSError, ValueError, KeyError):
+            pass
+    out = {"samples_per_launch": samples,
+           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC, separate passes, "
+                     "bench.py C3 workload; per launch (one launch per step)"}
+    for k in KERNELS:
+        if k not in fetch or k not in write:
+            continue
+        f_raw, w = fetch[k] * 1024, write[k] * 1024
+        out[f"{k}_fetch_bytes_raw"] = round(f_raw)
+        out[f"{k}_write_bytes"] = round(w)
+        out[f"{k}_bytes_per_launch"] = round(2 * f_raw + w)
+        if k in atom:
+            out[f"{k}_atomic_requests"] = round(atom[k])
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+if __name__ == "__main__":
+    main()
