@@ -128,21 +128,25 @@ int rn_ml_composite_bw(const float* dL_drgb, const float* dL_dopacity, const flo
  * level_* (16 entries) and xyz_min/extent (3) are HOST arrays read at launch;
  * frags = packed f16 weights (device).
  * rn_field_bwd ADDS into grid_grad (fp32, tcnn layout) and dw (fp32, K x
- * FIELD_PARAMS); the caller zeroes them when a fresh gradient is wanted.    */
+ * FIELD_PARAMS); the caller zeroes them when a fresh gradient is wanted.
+ * feat_cache (optional, device, 64 B per sample slot = 32 f16 encodings,
+ * indexed like the samples): rn_field_fwd writes the hash-grid encoding there
+ * and rn_field_bwd reads it instead of re-gathering the grid.  Pass the same
+ * buffer and sample layout to both, or NULL to both.                       */
 int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
                  const int32_t* ray_of, const float* rays_o, const float* rays_d,
                  const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
                  const float* extent, const void* frags, float* sigma, float* rgb,
-                 int32_t blocks_per_model, void* stream);
+                 void* feat_cache, int32_t blocks_per_model, void* stream);
 int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
                  const int32_t* ray_of, const float* rays_o, const float* rays_d,
                  const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
                  const float* extent, const void* frags, const float* dL_dsigma,
-                 const float* dL_drgb, float* grid_grad, float* dw,
+                 const float* dL_drgb, float* grid_grad, float* dw, const void* feat_cache,
                  int32_t blocks_per_model, void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------

@@ -52,6 +52,7 @@ struct FieldArgs {
     float* dw;                // [K][FIELD_PARAMS]
     float* sigma; float* rgb; // forward outputs
     const float* dsigma; const float* drgb;               // backward seeds
+    rn_half* feat;            // optional encoding cache: [sample tiles][64 lanes][16] f16
     float xyz_min[3]; float extent[3];
     uint32_t grid_bytes;      // byte size of the f16 table (= of the f32 grad / 2)
     int dbg;                  // ablation flags (rn_set_debug_flags), 0 in production
@@ -291,7 +292,9 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-template <int MODE>
+enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2 };
+
+template <int MODE, int CACHE>
 __device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T, const rn_half* W,
                                              int64_t base, int64_t n, int64_t tile, FwdState& st,
                                              bool& valid, int64_t& s, float& ux, float& uy,
@@ -305,12 +308,24 @@ __device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T,
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-    encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
+    // the encoding cache is indexed by 32-sample tile of the global sample
+    // array (segment bases are 128-aligned); lane-linear, 32 B per lane
+    half8* fc = CACHE == CACHE_NONE ? nullptr
+              : reinterpret_cast<half8*>(a.feat) + (((base >> 5) + tile) * 64 + lane) * 2;
+    if (CACHE == CACHE_READ) {
+        // lanes past the segment end (the backward walks whole 8-tile
+        // iterations) were never written: zero encoding, as the gather path
+        st.e0 = rn_zero8(); st.e1 = rn_zero8();
+        if (valid) { st.e0 = fc[0]; st.e1 = fc[1]; }
+    } else {
+        encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
+        if (CACHE == CACHE_WRITE) { fc[0] = st.e0; fc[1] = st.e1; }
+    }
     st.sh = sh_lane(dx, dy, dz, h);
     mlp_forward(W, st);
 }
 
-template <int MODE>
+template <int MODE, int CACHE>
 __global__ void __launch_bounds__(256, FWD_MIN_WAVES)
 k_field_fwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FWD_FRAGS * RN_FRAG_HALFS];
@@ -330,7 +345,7 @@ k_field_fwd(FieldArgs a) {
         rn_lds_order();   // weights stay in LDS: no hoisting of fragment reads
         FwdState st;
         bool valid; int64_t s; float ux, uy, uz;
-        tile_forward<MODE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
+        tile_forward<MODE, CACHE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
         if (valid && h == 0) {
             // TruncExp.forward on the f16 geo output (custom_functions.py:165-167)
             a.sigma[s] = expf(st.g0);
@@ -515,7 +530,7 @@ __device__ __forceinline__ void dw_flush(const f32x16& acc, float* dw, int off, 
     }
 }
 
-template <int MODE>
+template <int MODE, int CACHE>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
 k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
@@ -565,7 +580,7 @@ k_field_bwd(FieldArgs a) {
         const int64_t tile = it * BWD_WAVES + wid;
         FwdState st;
         bool valid; int64_t s; float ux, uy, uz;
-        tile_forward<MODE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
+        tile_forward<MODE, CACHE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
 
         // ---- seeds (lanes h == 0 own the output rows)
         float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
@@ -787,26 +802,28 @@ int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
                  const float* extent, const void* frags, float* sigma, float* rgb,
-                 int32_t blocks_per_model, void* stream) {
+                 void* feat_cache, int32_t blocks_per_model, void* stream) {
     RN_CHECK_ARG(n_models >= 1 && n_samples >= 0 && blocks_per_model >= 1, "bad sizes");
     RN_CHECK_ARG(grid_f16 && level_offset && level_hsize && level_res && level_scale && xyz_min &&
                  extent && frags && sigma && rgb, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
-    a.sigma = sigma; a.rgb = rgb;
+    a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
     dim3 grid(blocks_per_model, n_models);
     if (xyzs) {
         RN_CHECK_ARG(dirs && n_models == 1, "xyz mode needs dirs and a single model");
         if (n_samples == 0) return 0;
         a.xyzs = xyzs; a.dirs = dirs; a.n_fixed = n_samples;
-        k_field_fwd<0><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+        if (feat_cache) k_field_fwd<0, CACHE_WRITE><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+        else k_field_fwd<0, CACHE_NONE><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     } else {
         RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count,
                      "compact mode needs ts/ray_of/rays/segments");
         a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
         a.seg_base = seg_base; a.seg_count = seg_count;
-        k_field_fwd<1><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+        if (feat_cache) k_field_fwd<1, CACHE_WRITE><<<grid, 256, 0, (hipStream_t)stream>>>(a);
+        else k_field_fwd<1, CACHE_NONE><<<grid, 256, 0, (hipStream_t)stream>>>(a);
     }
     RN_CHECK_LAUNCH();
     return 0;
@@ -818,7 +835,7 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  const void* grid_f16, const uint32_t* level_offset, const uint32_t* level_hsize,
                  const uint32_t* level_res, const float* level_scale, const float* xyz_min,
                  const float* extent, const void* frags, const float* dL_dsigma,
-                 const float* dL_drgb, float* grid_grad, float* dw,
+                 const float* dL_drgb, float* grid_grad, float* dw, const void* feat_cache,
                  int32_t blocks_per_model, void* stream) {
     RN_CHECK_ARG(n_models >= 1 && n_samples >= 0 && blocks_per_model >= 1, "bad sizes");
     RN_CHECK_ARG(grid_f16 && level_offset && level_hsize && level_res && level_scale && xyz_min &&
@@ -828,18 +845,21 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
     a.dbg = g_field_dbg;
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
+    a.feat = (rn_half*)feat_cache;
     dim3 grid(blocks_per_model, n_models);
     if (xyzs) {
         RN_CHECK_ARG(dirs && n_models == 1, "xyz mode needs dirs and a single model");
         if (n_samples == 0) return 0;
         a.xyzs = xyzs; a.dirs = dirs; a.n_fixed = n_samples;
-        k_field_bwd<0><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+        if (feat_cache) k_field_bwd<0, CACHE_READ><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+        else k_field_bwd<0, CACHE_NONE><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     } else {
         RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count,
                      "compact mode needs ts/ray_of/rays/segments");
         a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
         a.seg_base = seg_base; a.seg_count = seg_count;
-        k_field_bwd<1><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+        if (feat_cache) k_field_bwd<1, CACHE_READ><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
+        else k_field_bwd<1, CACHE_NONE><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     }
     RN_CHECK_LAUNCH();
     return 0;

@@ -35,8 +35,8 @@ SIGNATURES = {
     "rn_ml_combine_fw": [P, P, P, P, P, I64, I32, P, P, P, P],
     "rn_ml_combine_bw": [P, P, P, P, P, I64, I32, P, P],
     "rn_ml_composite_bw": [P, P, P, P, P, P, P, P, P, P, P, P, P, P, I64, I32, F32, P, P, P],
-    "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, I32, P],
-    "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P,
+    "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, I32, P],
+    "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                      I32, P],
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, P, I32, I32, P],

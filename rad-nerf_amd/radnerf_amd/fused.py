@@ -52,6 +52,8 @@ class Workspace:
         self.depth_k = torch.empty(K, B, **f)
         self.rgb_k = torch.empty(K, B, 3, **f)
         self.dgate = torch.empty(B, K, **f)
+        # field fwd -> bwd encoding cache: 32 f16 per sample slot (64 B)
+        self.feat = torch.empty((cap + 31) // 32 * 32, 32, device=device, dtype=torch.float16)
 
     @property
     def seg_base(self):
@@ -83,6 +85,7 @@ class FusedMLRenderer:
         self.bitfield_bytes = bf[0].numel()
         self.fwd_blocks = fwd_blocks or max(1, 2048 // K)
         self.bwd_blocks = bwd_blocks or max(1, 256 // K)
+        self.feat_cache = True      # field fwd stores the encoding, bwd skips the re-gather
         self.trace = False          # record HIP events around every launch
         self.events = {}
 
@@ -156,10 +159,11 @@ class FusedMLRenderer:
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
         if fwd:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
-                     self.fwd_blocks, st)
+                     w.feat.data_ptr() if self.feat_cache else None, self.fwd_blocks, st)
         else:
             self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
-                     w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(), self.bwd_blocks, st)
+                     w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),
+                     w.feat.data_ptr() if self.feat_cache else None, self.bwd_blocks, st)
 
     # ----------------------------------------------------------------- backward
     def backward(self, rays_o, rays_d, gate_in2, gate, bg, dL_drgb, dL_dopacity, dL_ddepth,

@@ -193,15 +193,15 @@ class MNGP(nn.Module):
             nb = blocks or max(1, min(2048, (n + 127) // 128))
             lib().field_fwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
                             None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
-                            self._h_ext.ctypes.data, fptr, sigma.data_ptr(), rgb.data_ptr(), nb,
-                            _stream(dev))
+                            self._h_ext.ctypes.data, fptr, sigma.data_ptr(), rgb.data_ptr(), None,
+                            nb, _stream(dev))
         else:
             nb = blocks or max(1, min(256, (n + 255) // 256))
             lib().field_bwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
                             None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
                             self._h_ext.ctypes.data, fptr, dsigma.data_ptr(), drgb.data_ptr(),
-                            grid_grad.data_ptr(), dw.data_ptr() + ind * LY.FIELD_PARAMS * 4, nb,
-                            _stream(dev))
+                            grid_grad.data_ptr(), dw.data_ptr() + ind * LY.FIELD_PARAMS * 4, None,
+                            nb, _stream(dev))
 
     # ------------------------------------------------------------ reference API
     def density(self, x, ind, return_feat=False):
