@@ -182,7 +182,7 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
                 const uint32_t idx = corner_index(lc, P[u], c);
-                off[8 * u + c] = valid ? 4u * (lc.off + idx) : RN_OOB;
+                off[8 * u + c] = (valid && !(a.dbg & 128)) ? 4u * (lc.off + idx) : RN_OOB;
             }
         }
         uint32_t raw[16];
@@ -318,7 +318,8 @@ __device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T,
         st.e0 = rn_zero8(); st.e1 = rn_zero8();
         if (valid) { st.e0 = fc[0]; st.e1 = fc[1]; }
     } else {
-        encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
+        if (a.dbg & 256) { st.e0 = rn_zero8(); st.e1 = rn_zero8(); asm volatile("" :: "v"(ux), "v"(uy), "v"(uz)); }
+        else encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
         if (CACHE == CACHE_WRITE) { fc[0] = st.e0; fc[1] = st.e1; }
     }
     st.sh = sh_lane(dx, dy, dz, h);
@@ -810,6 +811,7 @@ int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
+    a.dbg = g_field_dbg;
     dim3 grid(blocks_per_model, n_models);
     if (xyzs) {
         RN_CHECK_ARG(dirs && n_models == 1, "xyz mode needs dirs and a single model");

@@ -84,30 +84,114 @@ __device__ __forceinline__ bool march_step(float& t, float ox, float oy, float o
     return false;
 }
 
-// Pass 1 (COUNT) or pass 2 (write) of raymarching.cu:200-279 for one ray.
-template <bool COUNT, typename Sink>
-__device__ int march_ray(float ox, float oy, float oz, float dx, float dy, float dz,
-                         float t1, float t2, int n_write, int start,
-                         const uint8_t* __restrict__ bitfield, const MarchCfg& c,
-                         const Sink& sink) {
+// Occupancy query of raymarching.cu:205-224 at t: occupied?  If not, the skip
+// target of :225-230 (exit of the cell at its mip level).
+__device__ __forceinline__ bool march_query(float t, float ox, float oy, float oz,
+                                            float dx, float dy, float dz,
+                                            float dxi, float dyi, float dzi,
+                                            const uint8_t* __restrict__ bitfield,
+                                            const MarchCfg& c, float& x, float& y, float& z,
+                                            float& dt, float& t_target) {
+    const uint32_t g3 = (uint32_t)c.grid_size * c.grid_size * c.grid_size;
+    const float gsi = 1.0f / c.grid_size;
+    x = fmaf(t, dx, ox); y = fmaf(t, dy, oy); z = fmaf(t, dz, oz);
+    dt = rn_calc_dt(t, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+    const int mip = max(rn_mip_from_pos(x, y, z, c.cascades),
+                        rn_mip_from_dt(dt, c.grid_size, c.cascades));
+    const float mb = fminf(scalbnf(1.0f, mip - 1), c.scale);
+    const float mbi = 1 / mb;
+    const float gm1 = c.grid_size - 1.0f;
+    const int nx = (int)rn_clampf(0.5f * fmaf(x, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const int ny = (int)rn_clampf(0.5f * fmaf(y, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const int nz = (int)rn_clampf(0.5f * fmaf(z, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
+    const uint32_t idx = mip * g3 + rn_morton3d(nx, ny, nz);
+    const bool occ = bitfield[idx / 8] & (1 << (idx % 8));
+    const float tx = fmaf(fmaf(fmaf(0.5f, rn_signf(dx), nx + 0.5f) * gsi, 2.0f, -1.0f), mb, -x) * dxi;
+    const float ty = fmaf(fmaf(fmaf(0.5f, rn_signf(dy), ny + 0.5f) * gsi, 2.0f, -1.0f), mb, -y) * dyi;
+    const float tz = fmaf(fmaf(fmaf(0.5f, rn_signf(dz), nz + 0.5f) * gsi, 2.0f, -1.0f), mb, -z) * dzi;
+    t_target = t + fmaxf(0.0f, fminf(tx, fminf(ty, tz)));
+    return occ;
+}
+
+// One ray marched by a whole wave (raymarching.cu:200-279, bit-exact).
+//
+// The reference marches a ray serially: at the current t it queries the cell;
+// occupied -> emit, t += dt(t); empty -> repeat t += dt(t) until t >= the
+// cell's exit.  Either way t only ever advances by t += dt(t), so the values
+// t_k visited form ONE fixed sequence; occupancy only decides which k are
+// queried (the chain) and emitted.  The wave evaluates 64 consecutive t_k per
+// chunk (lane j: t_{base+j}, the same float additions in the same order),
+// queries all of them in parallel (one bitfield load per lane instead of one
+// dependent load per step), and then walks the chain through the chunk with
+// scalar ops: next(k) = k + 1 if occupied, else the first k' > k with
+// t_k' >= target(k) (the do-while of :228-230).  The chain is the reference's
+// sequence of queries, so counts and samples are identical; the serial
+// latency per step drops from a dependent L2 load to a few scalar ops.
+template <bool WRITE, typename Sink>
+__device__ int march_ray_wave(float ox, float oy, float oz, float dx, float dy, float dz,
+                              float t1, float t2, int cap, int start,
+                              const uint8_t* __restrict__ bitfield, const MarchCfg& c,
+                              const Sink& sink) {
+    const int lane = rn_lane();
+    if (!(0.0f <= t1 && t1 < t2) || cap <= 0) return 0;
     const float dxi = 1.0f / dx, dyi = 1.0f / dy, dzi = 1.0f / dz;
-    float t = t1;
+    const uint64_t lt_mask = (1ull << lane) - 1ull;
+    float tb = t1;                 // t at the chunk's first step (wave-uniform)
+    float need = -INFINITY;        // chain resumes at the first step with t >= need
     int n = 0;
-    if (COUNT) {
-        while (0 <= t && t < t2 && n < c.max_samples) {
-            float x, y, z, dt;
-            if (march_step(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c, x, y, z, dt)) {
-                t += dt; n++;
+    while (true) {
+        float t = tb;
+        if (c.esf == 0.0f) {            // constant dt (scale <= 0.5 scenes): same adds, no clamp
+            const float d0 = rn_calc_dt(0.0f, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+#pragma unroll 16
+            for (int i = 0; i < RN_WAVE - 1; ++i) { const float nt = t + d0; t = i < lane ? nt : t; }
+        } else {
+#pragma unroll 8
+            for (int i = 0; i < RN_WAVE - 1; ++i) {
+                const float nt = t + rn_calc_dt(t, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+                t = i < lane ? nt : t;
             }
         }
-    } else {
-        while (t < t2 && n < n_write) {
-            float x, y, z, dt;
-            if (march_step(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c, x, y, z, dt)) {
-                sink.emit(start + n, x, y, z, t, dt);
-                t += dt; n++;
+        const bool alive = t < t2;                      // a prefix of the lanes
+        float x, y, z, dt, target;
+        const bool occ = march_query(t, ox, oy, oz, dx, dy, dz, dxi, dyi, dzi, bitfield, c,
+                                     x, y, z, dt, target) && alive;
+        const uint64_t alive_m = __builtin_amdgcn_ballot_w64(alive);
+        const uint64_t occ_m = __builtin_amdgcn_ballot_w64(occ);
+        // walk the chain through this chunk (scalar).  A run of occupied steps
+        // is on the chain as a whole (next(k) = k + 1), so one iteration per
+        // run and one per empty query.
+        uint64_t mark = 0;
+        const uint64_t cand = __builtin_amdgcn_ballot_w64(alive && t >= need);
+        int cur = cand ? __builtin_ctzll(cand) : RN_WAVE;
+        int emitted = 0;
+        bool full = false;
+        while (cur < RN_WAVE) {
+            const uint64_t from = ~0ull << cur;
+            if ((occ_m >> cur) & 1ull) {
+                const uint64_t stop = ~occ_m & from;
+                int end = stop ? __builtin_ctzll(stop) : RN_WAVE;
+                if (n + emitted + (end - cur) >= cap) { end = cur + (cap - n - emitted); full = true; }
+                mark |= from & (end < RN_WAVE ? ~(~0ull << end) : ~0ull);
+                emitted += end - cur;
+                need = -INFINITY;
+                if (full) break;
+                cur = (end < RN_WAVE && ((alive_m >> end) & 1ull)) ? end : RN_WAVE;
+            } else {
+                mark |= 1ull << cur;
+                need = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(target), cur));
+                const uint64_t nxt = __builtin_amdgcn_ballot_w64(alive && t >= need) & (from << 1);
+                cur = nxt ? __builtin_ctzll(nxt) : RN_WAVE;
             }
         }
+        const uint64_t emit_m = mark & occ_m;
+        if (WRITE && ((emit_m >> lane) & 1ull))
+            sink.emit(start + n + __builtin_popcountll(emit_m & lt_mask), x, y, z, t, dt);
+        n += __builtin_popcountll(emit_m);
+        if (full || alive_m != ~0ull) break;            // cap reached, or the ray left [t1, t2)
+        const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), RN_WAVE - 1));
+        tb = tl + rn_calc_dt(tl, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+        if (!(tb < t2)) break;
     }
     return n;
 }
@@ -140,12 +224,14 @@ __global__ void __launch_bounds__(256)
 k_march_train_count(int n_rays, const float* __restrict__ rays_o, const float* __restrict__ rays_d,
                     const float* __restrict__ hits_t, const float* __restrict__ noise,
                     const uint8_t* __restrict__ bitfield, MarchCfg c, int32_t* __restrict__ counts) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;   // one wave per ray
     if (r >= n_rays) return;
     const float t1 = perturbed_t1(hits_t[2 * r], noise[r], c);
-    counts[r] = march_ray<true>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2],
-                                rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2],
-                                t1, hits_t[2 * r + 1], 0, 0, bitfield, c, NoSink{});
+    const int n = march_ray_wave<false>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2],
+                                        rays_d[3 * r], rays_d[3 * r + 1], rays_d[3 * r + 2],
+                                        t1, hits_t[2 * r + 1], c.max_samples, 0, bitfield, c,
+                                        NoSink{});
+    if (rn_lane() == 0) counts[r] = n;
 }
 
 __global__ void __launch_bounds__(256)
@@ -155,16 +241,16 @@ k_march_train_write(int n_rays, const float* __restrict__ rays_o, const float* _
                     const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
                     int64_t* __restrict__ rays_a, float* __restrict__ xyzs,
                     float* __restrict__ dirs, float* __restrict__ deltas, float* __restrict__ ts) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int r = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;   // one wave per ray
     if (r >= n_rays) return;
     const int n = counts[r], start = offsets[r];
-    rays_a[3 * r + 0] = r; rays_a[3 * r + 1] = start; rays_a[3 * r + 2] = n;
+    if (rn_lane() == 0) { rays_a[3 * r + 0] = r; rays_a[3 * r + 1] = start; rays_a[3 * r + 2] = n; }
     if (n == 0) return;
     const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
     const float t1 = perturbed_t1(hits_t[2 * r], noise[r], c);
     RefSink sink{xyzs, dirs, ts, deltas, dx, dy, dz};
-    march_ray<false>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2], dx, dy, dz,
-                     t1, hits_t[2 * r + 1], n, start, bitfield, c, sink);
+    march_ray_wave<true>(rays_o[3 * r], rays_o[3 * r + 1], rays_o[3 * r + 2], dx, dy, dz,
+                         t1, hits_t[2 * r + 1], n, start, bitfield, c, sink);
 }
 
 // ----------------------------------------------------------------------------
@@ -223,7 +309,7 @@ k_ml_march_count(int n_rays, int K, const float* __restrict__ rays_o,
                  const float* __restrict__ half_size, float near_distance,
                  const float* __restrict__ noise, const uint8_t* __restrict__ bitfields,
                  int64_t bitfield_bytes, MarchCfg c, int32_t* __restrict__ counts) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gid = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;  // wave per (k, ray)
     if (gid >= n_rays * K) return;
     const int k = gid / n_rays, r = gid - k * n_rays;
     const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
@@ -233,8 +319,9 @@ k_ml_march_count(int n_rays, int K, const float* __restrict__ rays_o,
     if (!(t2 > 0)) { t1 = -1.0f; t2 = -1.0f; }              // intersection.cu:48
     else { t1 = fmaxf(t1, 0.0f); if (t1 < near_distance) t1 = near_distance; }
     t1 = perturbed_t1(t1, noise[gid], c);
-    counts[gid] = march_ray<true>(ox, oy, oz, dx, dy, dz, t1, t2, 0, 0,
-                                  bitfields + (size_t)k * bitfield_bytes, c, NoSink{});
+    const int n = march_ray_wave<false>(ox, oy, oz, dx, dy, dz, t1, t2, c.max_samples, 0,
+                                        bitfields + (size_t)k * bitfield_bytes, c, NoSink{});
+    if (rn_lane() == 0) counts[gid] = n;
 }
 
 __global__ void __launch_bounds__(256)
@@ -245,7 +332,7 @@ k_ml_march_write(int n_rays, int K, const float* __restrict__ rays_o,
                  int64_t bitfield_bytes, MarchCfg c, const int32_t* __restrict__ counts,
                  const int32_t* __restrict__ offsets, float* __restrict__ ts,
                  float* __restrict__ deltas, int32_t* __restrict__ ray_of) {
-    const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gid = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;  // wave per (k, ray)
     if (gid >= n_rays * K) return;
     const int n = counts[gid];
     if (n == 0) return;
@@ -258,8 +345,8 @@ k_ml_march_write(int n_rays, int K, const float* __restrict__ rays_o,
     if (t1 < near_distance) t1 = near_distance;
     t1 = perturbed_t1(t1, noise[gid], c);
     CompactSink sink{ts, deltas, ray_of, r};
-    march_ray<false>(ox, oy, oz, dx, dy, dz, t1, t2, n, offsets[gid],
-                     bitfields + (size_t)k * bitfield_bytes, c, sink);
+    march_ray_wave<true>(ox, oy, oz, dx, dy, dz, t1, t2, n, offsets[gid],
+                         bitfields + (size_t)k * bitfield_bytes, c, sink);
 }
 
 // ----------------------------------------------------------------------------
@@ -380,7 +467,7 @@ int rn_raymarching_train_count(const float* rays_o, const float* rays_d, const f
     if (n_rays == 0) return 0;
     RN_CHECK_ARG(rays_o && rays_d && hits_t && density_bitfield && noise && counts, "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    k_march_train_count<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+    k_march_train_count<<<nblk(n_rays, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, rays_o, rays_d, hits_t, noise, density_bitfield, c, counts);
     RN_CHECK_LAUNCH();
     return 0;
@@ -408,7 +495,7 @@ int rn_raymarching_train_write(const float* rays_o, const float* rays_d, const f
     RN_CHECK_ARG(rays_o && rays_d && hits_t && density_bitfield && noise && counts && offsets &&
                  rays_a, "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    k_march_train_write<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+    k_march_train_write<<<nblk(n_rays, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, rays_o, rays_d, hits_t, noise, density_bitfield, c, counts, offsets, rays_a,
         xyzs, dirs, deltas, ts);
     RN_CHECK_LAUNCH();
@@ -449,7 +536,7 @@ int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* cen
     RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts,
                  "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    k_ml_march_count<<<nblk(n_rays * n_models, 256), 256, 0, (hipStream_t)stream>>>(
+    k_ml_march_count<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
         density_bitfields, bitfield_bytes, c, counts);
     RN_CHECK_LAUNCH();
@@ -469,7 +556,7 @@ int rn_ml_march_write(const float* rays_o, const float* rays_d, const float* cen
     RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts &&
                  offsets && ts && deltas && ray_of, "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    k_ml_march_write<<<nblk(n_rays * n_models, 256), 256, 0, (hipStream_t)stream>>>(
+    k_ml_march_write<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
         density_bitfields, bitfield_bytes, c, counts, offsets, ts, deltas, ray_of);
     RN_CHECK_LAUNCH();

@@ -39,14 +39,18 @@ def main():
     r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
     L = lib()
     st = torch.cuda.current_stream().cuda_stream
+    # tokens: "<flags>" = field_bwd with debug flags, "f<flags>" = field_fwd
     times = {f: [] for f in flags}
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(int(f))
+            L.set_debug_flags(int(f.lstrip("f")))
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            r._field(False, o, d, st, gg, mg)
+            if f.startswith("f"):
+                r._field(True, o, d, st)
+            else:
+                r._field(False, o, d, st, gg, mg)
             b.record()
             torch.cuda.synchronize()
             times[f].append(a.elapsed_time(b))
@@ -58,7 +62,10 @@ def main():
         torch.cuda.synchronize()
         fwd.append(a.elapsed_time(b))
     out = {"samples": r.ws.n_samples(), "field_fwd_ms": float(np.median(fwd)),
-           "field_bwd_ms": {str(f): float(np.median(v)) for f, v in times.items()}}
+           "field_bwd_ms": {str(f): float(np.median(v)) for f, v in times.items()
+                            if not f.startswith("f")},
+           "field_fwd_flags_ms": {str(f): float(np.median(v)) for f, v in times.items()
+                                  if f.startswith("f")}}
     print(json.dumps(out))
 
 
