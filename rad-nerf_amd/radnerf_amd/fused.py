@@ -89,16 +89,23 @@ class FusedMLRenderer:
         self.trace = False          # record HIP events around every launch
         self.events = {}
 
-    def _ev(self, name, L_call, *args):
+    def _ev(self, name, L_call, *args, stream=None):
         """Launch through librn; with tracing on, bracket it with events on the
         launch stream (bench.py's per-kernel timing)."""
         if not self.trace:
             return L_call(*args)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
+        a.record(stream)
         L_call(*args)
-        b.record()
+        b.record(stream)
         self.events.setdefault(name, []).append((a, b))
+
+    def _side(self, dev):
+        """Side stream for the gate MLP: it runs beside the march (forward) and
+        beside field_bwd (backward), joined back before its outputs are used."""
+        if getattr(self, "_side_stream", None) is None:
+            self._side_stream = torch.cuda.Stream(dev)
+        return self._side_stream
 
     def kernel_times_ms(self):
         """{kernel: [ms per launch]} of the traced launches (synchronises)."""
@@ -122,9 +129,13 @@ class FusedMLRenderer:
         st = _stream(rays_o.device)
         out_gate = torch.empty(B, K, device=rays_o.device)
         imp = torch.zeros(K, device=rays_o.device)
+        side = self._side(rays_o.device)
+        main = torch.cuda.current_stream(rays_o.device)
+        frags = g.packed_frags()          # (re)packed on the main stream
+        side.wait_stream(main)
         self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
-                 g.packed_frags().data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
-                 max(1, min(256, (B + 127) // 128)), st)
+                 frags.data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
+                 max(1, min(256, (B + 127) // 128)), side.cuda_stream, stream=side)
         bits = self.bitfields()
         march = (rays_o.data_ptr(), rays_d.data_ptr(), m.center.data_ptr(),
                  m.half_size.data_ptr(), NEAR_DISTANCE, noise.data_ptr(), bits.data_ptr(),
@@ -145,6 +156,9 @@ class FusedMLRenderer:
         rgb = torch.empty(B, 3, device=rays_o.device)
         opacity = torch.empty(B, device=rays_o.device)
         depth = torch.empty(B, K, device=rays_o.device)
+        main.wait_stream(side)            # gate output joins here
+        out_gate.record_stream(side)
+        imp.record_stream(side)
         self._ev("combine_fw", L.ml_combine_fw, out_gate.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
                         w.rgb_k.data_ptr(), bg.data_ptr(), B, K, rgb.data_ptr(),
                         opacity.data_ptr(), depth.data_ptr(), st)
@@ -189,11 +203,18 @@ class FusedMLRenderer:
                           w.offsets.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
                           w.rgb_k.data_ptr(), B, K, float(T_threshold), w.dsigma.data_ptr(),
                           w.drgb.data_ptr(), st)
-        self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
+        # gate backward beside field_bwd: it only needs dL/dgate (combine_bw)
+        side = self._side(dev)
+        main = torch.cuda.current_stream(dev)
+        frags, dwm = g.packed_frags(), g.dw_map(dev)
+        side.wait_stream(main)
         self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
-                 g.packed_frags().data_ptr(),
-                   g.dw_map(dev).data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
-                   gate_grad.numel(), max(1, min(128, (B + 127) // 128)), st)
+                 frags.data_ptr(), dwm.data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
+                 gate_grad.numel(), max(1, min(128, (B + 127) // 128)), side.cuda_stream,
+                 stream=side)
+        self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
+        main.wait_stream(side)
+        gate_grad.record_stream(side)
         return grid_grad, mlp_grad, gate_grad
 
 
