@@ -68,12 +68,20 @@ int rn_raymarching_test(const float* rays_o, const float* rays_d, float* hits_t,
 
 /* ---- fused multi-sub-NeRF march (ml_rendering.py:47-52 + :174-179) -------
  * AABB + NEAR clamp + jitter + march for K models in one launch; counts and
- * noise are [K][n_rays]; writes compact samples (t, dt, ray).               */
+ * noise are [K][n_rays]; writes compact samples (t, dt, ray).
+ * Two-pass form: rn_ml_march_count -> rn_scan_segments -> rn_ml_march_write.
+ * Single-pass form: rn_ml_march_count with stage_ts/stage_deltas (K*n_rays*
+ * max_samples floats each; slot of (k, r) at (k*n_rays + r)*max_samples) ->
+ * rn_scan_segments -> rn_ml_compact.                                       */
 int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* center,
                       const float* half_size, float near_distance, const float* noise,
                       const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
                       int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
-                      int32_t max_samples, int64_t n_rays, int32_t* counts, void* stream);
+                      int32_t max_samples, int64_t n_rays, int32_t* counts, float* stage_ts,
+                      float* stage_deltas, void* stream);
+int rn_ml_compact(const int32_t* counts, const int32_t* offsets, int64_t n_rays, int32_t n_models,
+                  int32_t max_samples, const float* stage_ts, const float* stage_deltas,
+                  float* ts, float* deltas, int32_t* ray_of, void* stream);
 int rn_ml_march_write(const float* rays_o, const float* rays_d, const float* center,
                       const float* half_size, float near_distance, const float* noise,
                       const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,

@@ -28,7 +28,7 @@
 #define FIELD_PARAMS 9472
 #define FIELD_DW_TILES 12
 #ifndef FWD_MIN_WAVES
-#define FWD_MIN_WAVES 3
+#define FWD_MIN_WAVES 2
 #endif
 
 struct GridMeta {
@@ -204,7 +204,9 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
         }
         // keep at most one batch of gathers in flight per wave: bounds VGPRs so
         // more waves fit (TLP hides the L2/MALL latency instead of ILP)
+#ifndef FWD_NO_SCHED_BARRIER
         __builtin_amdgcn_sched_barrier(0);
+#endif
     }
     // element j of k-step s <-> level lane_level(4s + (j>>1), h), feature j&1
 #pragma unroll

@@ -42,6 +42,15 @@ struct RefSink {
     }
 };
 
+// staging sink of the single-pass fused march: per-(model, ray) slots of
+// max_samples records (t, dt), compacted after the scan by k_ml_compact
+struct StageSink {
+    float* __restrict__ ts; float* __restrict__ deltas;
+    __device__ __forceinline__ void emit(int s, float, float, float, float t, float dt) const {
+        ts[s] = t; deltas[s] = dt;
+    }
+};
+
 // compact sink for the fused path: t, dt and owning ray
 struct CompactSink {
     float* __restrict__ ts; float* __restrict__ deltas; int32_t* __restrict__ ray_of;
@@ -303,12 +312,14 @@ k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ cou
 // :174-179): AABB + NEAR clamp + jitter + count for K sub-NeRFs in one launch.
 // thread -> (k, r); bitfields: [K][bitfield_bytes]; noise: [K][B]
 // ----------------------------------------------------------------------------
+template <bool STAGE>
 __global__ void __launch_bounds__(256)
 k_ml_march_count(int n_rays, int K, const float* __restrict__ rays_o,
                  const float* __restrict__ rays_d, const float* __restrict__ center,
                  const float* __restrict__ half_size, float near_distance,
                  const float* __restrict__ noise, const uint8_t* __restrict__ bitfields,
-                 int64_t bitfield_bytes, MarchCfg c, int32_t* __restrict__ counts) {
+                 int64_t bitfield_bytes, MarchCfg c, int32_t* __restrict__ counts,
+                 float* __restrict__ stage_ts, float* __restrict__ stage_dt) {
     const int gid = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;  // wave per (k, ray)
     if (gid >= n_rays * K) return;
     const int k = gid / n_rays, r = gid - k * n_rays;
@@ -319,9 +330,33 @@ k_ml_march_count(int n_rays, int K, const float* __restrict__ rays_o,
     if (!(t2 > 0)) { t1 = -1.0f; t2 = -1.0f; }              // intersection.cu:48
     else { t1 = fmaxf(t1, 0.0f); if (t1 < near_distance) t1 = near_distance; }
     t1 = perturbed_t1(t1, noise[gid], c);
-    const int n = march_ray_wave<false>(ox, oy, oz, dx, dy, dz, t1, t2, c.max_samples, 0,
-                                        bitfields + (size_t)k * bitfield_bytes, c, NoSink{});
+    int n;
+    if (STAGE)
+        n = march_ray_wave<true>(ox, oy, oz, dx, dy, dz, t1, t2, c.max_samples,
+                                 gid * c.max_samples, bitfields + (size_t)k * bitfield_bytes, c,
+                                 StageSink{stage_ts, stage_dt});
+    else
+        n = march_ray_wave<false>(ox, oy, oz, dx, dy, dz, t1, t2, c.max_samples, 0,
+                                  bitfields + (size_t)k * bitfield_bytes, c, NoSink{});
     if (rn_lane() == 0) counts[gid] = n;
+}
+
+// staged samples -> compact model-major layout at the scanned offsets
+__global__ void __launch_bounds__(256)
+k_ml_compact(int n_rays, int K, int max_samples, const int32_t* __restrict__ counts,
+             const int32_t* __restrict__ offsets, const float* __restrict__ stage_ts,
+             const float* __restrict__ stage_dt, float* __restrict__ ts,
+             float* __restrict__ deltas, int32_t* __restrict__ ray_of) {
+    const int gid = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;
+    if (gid >= n_rays * K) return;
+    const int r = gid % n_rays;
+    const int n = counts[gid], o = offsets[gid];
+    const size_t src = (size_t)gid * max_samples;
+    for (int i = rn_lane(); i < n; i += RN_WAVE) {
+        ts[o + i] = stage_ts[src + i];
+        deltas[o + i] = stage_dt[src + i];
+        ray_of[o + i] = r;
+    }
 }
 
 __global__ void __launch_bounds__(256)
@@ -527,18 +562,26 @@ int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* cen
                       const float* half_size, float near_distance, const float* noise,
                       const uint8_t* density_bitfields, int64_t bitfield_bytes, int32_t n_models,
                       int32_t cascades, float scale, float exp_step_factor, int32_t grid_size,
-                      int32_t max_samples, int64_t n_rays, int32_t* counts, void* stream) {
+                      int32_t max_samples, int64_t n_rays, int32_t* counts, float* stage_ts,
+                      float* stage_deltas, void* stream) {
     RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && cascades >= 1 && grid_size >= 1 &&
                  max_samples >= 1, "bad sizes");
+    RN_CHECK_ARG((stage_ts == nullptr) == (stage_deltas == nullptr), "stage_ts/stage_deltas: both or neither");
+    RN_CHECK_ARG(n_rays * n_models * (int64_t)max_samples < (int64_t)1 << 31, "staging too large");
     RN_CHECK_ARG(bitfield_bytes >= (int64_t)cascades * grid_size * grid_size * grid_size / 8,
                  "bitfield too small");
     if (n_rays == 0) return 0;
     RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts,
                  "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    k_ml_march_count<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
-        (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
-        density_bitfields, bitfield_bytes, c, counts);
+    if (stage_ts)
+        k_ml_march_count<true><<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
+            (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
+            density_bitfields, bitfield_bytes, c, counts, stage_ts, stage_deltas);
+    else
+        k_ml_march_count<false><<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
+            (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
+            density_bitfields, bitfield_bytes, c, counts, nullptr, nullptr);
     RN_CHECK_LAUNCH();
     return 0;
 }
@@ -559,6 +602,20 @@ int rn_ml_march_write(const float* rays_o, const float* rays_d, const float* cen
     k_ml_march_write<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,
         density_bitfields, bitfield_bytes, c, counts, offsets, ts, deltas, ray_of);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_ml_compact(const int32_t* counts, const int32_t* offsets, int64_t n_rays, int32_t n_models,
+                  int32_t max_samples, const float* stage_ts, const float* stage_deltas,
+                  float* ts, float* deltas, int32_t* ray_of, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && max_samples >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(counts && offsets && stage_ts && stage_deltas && ts && deltas && ray_of,
+                 "null pointer");
+    k_ml_compact<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, n_models, max_samples, counts, offsets, stage_ts, stage_deltas, ts, deltas,
+        ray_of);
     RN_CHECK_LAUNCH();
     return 0;
 }

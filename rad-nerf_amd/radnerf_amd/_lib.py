@@ -25,7 +25,9 @@ SIGNATURES = {
                                    P, P, P],
     "rn_scan_segments": [P, I32, I64, I32, P, P, P, P, P],
     "rn_raymarching_test": [P, P, P, P, I64, P, I32, F32, F32, I32, I32, I32, P, P, P, P, P, P],
-    "rn_ml_march_count": [P, P, P, P, F32, P, P, I64, I32, I32, F32, F32, I32, I32, I64, P, P],
+    "rn_ml_march_count": [P, P, P, P, F32, P, P, I64, I32, I32, F32, F32, I32, I32, I64, P, P, P,
+                          P],
+    "rn_ml_compact": [P, P, I64, I32, I32, P, P, P, P, P, P],
     "rn_ml_march_write": [P, P, P, P, F32, P, P, I64, I32, I32, F32, F32, I32, I32, I64, P, P,
                           P, P, P, P],
     "rn_composite_train_fw": [P, P, P, P, P, I64, F32, P, P, P, P, P, P],

@@ -2,7 +2,8 @@
 (models/ml_rendering.py:11-78 + :158-202) for all K sub-NeRFs as a fixed
 chain of HIP launches with no host synchronisation:
 
-  forward : gate_fwd -> ml_march_count -> scan_segments -> ml_march_write
+  forward : gate_fwd (side stream) | ml_march_count (single pass, staged)
+            -> scan_segments -> ml_compact
             -> field_fwd (all K models, compact samples) -> ml_composite_fw
             -> ml_combine_fw
   backward: ml_combine_bw -> ml_composite_bw -> field_bwd -> gate_bwd
@@ -52,6 +53,9 @@ class Workspace:
         self.depth_k = torch.empty(K, B, **f)
         self.rgb_k = torch.empty(K, B, 3, **f)
         self.dgate = torch.empty(B, K, **f)
+        # single-pass march staging: max_samples slots per (model, ray)
+        self.stage_ts = torch.empty(K * B * max_samples, **f)
+        self.stage_dt = torch.empty(K * B * max_samples, **f)
         # field fwd -> bwd encoding cache: 32 f16 per sample slot (64 B)
         self.feat = torch.empty((cap + 31) // 32 * 32, 32, device=device, dtype=torch.float16)
 
@@ -141,13 +145,16 @@ class FusedMLRenderer:
                  m.half_size.data_ptr(), NEAR_DISTANCE, noise.data_ptr(), bits.data_ptr(),
                  self.bitfield_bytes, K, m.cascades, float(m.scale), float(exp_step_factor),
                  m.grid_size, MAX_SAMPLES, B)
-        self._ev("march_count", L.ml_march_count, *march, w.counts.data_ptr(), st)
+        # single pass: march once into per-(model, ray) staging slots, scan the
+        # counts, compact (the two-pass form re-marches every ray instead)
+        self._ev("march", L.ml_march_count, *march, w.counts.data_ptr(),
+                 w.stage_ts.data_ptr(), w.stage_dt.data_ptr(), st)
         self._ev("scan", L.scan_segments, w.counts.data_ptr(), K, B, SEG_ALIGN,
                  w.offsets.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(),
                  w.meta.data_ptr(), st)
-        self._ev("march_write", L.ml_march_write, *march, w.counts.data_ptr(),
-                 w.offsets.data_ptr(), w.ts.data_ptr(), w.deltas.data_ptr(), w.ray_of.data_ptr(),
-                 st)
+        self._ev("compact", L.ml_compact, w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
+                 MAX_SAMPLES, w.stage_ts.data_ptr(), w.stage_dt.data_ptr(), w.ts.data_ptr(),
+                 w.deltas.data_ptr(), w.ray_of.data_ptr(), st)
         self._field(True, rays_o, rays_d, st)
         self._ev("composite_fw", L.ml_composite_fw, w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
                           w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
