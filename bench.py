@@ -41,6 +41,8 @@ FIELD_BWD_BYTES_PER_SAMPLE = 16 + 24 + 1024
 FIELD_FWD_BYTES_PER_SAMPLE = 24 + 512 + 16
 # whole path fwd+bwd: 612 + 1112
 PATH_BYTES_PER_SAMPLE = 1724
+MLP_FLOP_PER_SAMPLE = 56832          # fwd + bwd, SURVEY.md §8(d)
+MFMA_F16_PEAK_TFLOPS = 2500.0        # MI355X dense f16/bf16 (MI355X_MICROARCH.md)
 # MI355X_MICROARCH.md "Global float atomics": ~1.3 TB/s of added bytes at four
 # 64-B requests per 256-B wave instruction = 20.3 G requests/s chip-wide
 ATOMIC_PEAK_GREQ = 1.3e12 / 64 / 1e9
@@ -122,6 +124,26 @@ def main():
     elapsed = time.perf_counter() - t0
     r.trace = False
     kt = r.kernel_times_ms()
+
+    # forward-only rate (north_star's forward target), timed after the headline
+    # region with the same barrier/sync bracketing; not part of `value`
+    fwd_acc = torch.zeros((), dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        r.forward(rays_o, rays_d, rays_d, noises[i % 4], bg, 1e-4, esf)
+        fwd_acc.add_(r.ws.meta[1])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    fwd_elapsed = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(fwd_acc)
+        dist.all_reduce(fwd_elapsed, op=dist.ReduceOp.MAX)
+    fwd_only = {"value": round(int(fwd_acc) / float(fwd_elapsed) / 1e6, 2), "unit": "Msamples/s",
+                "ms_per_step": round(float(fwd_elapsed) / args.steps * 1e3, 4)}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:
@@ -184,6 +206,12 @@ def main():
                           "global_batch": B * world, "parallelism": f"dp{world}"},
                "roofline": roofline, "cpu_baseline": cpu_base,
                "rgb_linf_vs_ref": rgb_linf,
+               "forward_only": fwd_only,
+               # MFMA use: algorithmic MLP flops (56,832 per sample
+               # fwd+bwd, unpadded) at `value`, against the dense f16 peak
+               "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),
+                        "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6 / MFMA_F16_PEAK_TFLOPS, 5)},
                "kernel_ms": {k: round(v, 4) for k, v in sorted(kms.items())}}
         print(json.dumps(out), flush=True)
     if world > 1:
