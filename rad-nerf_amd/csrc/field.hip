@@ -164,43 +164,62 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rn_rsrc(const void* p, uint32_
 
 #define RN_OOB 0x80000000u   // buffer offset past num_records: load returns 0
 
-// hash-grid encoding of this lane's 8 levels -> the two B fragments.
-// Two levels (16 corner gathers) in flight per batch, 32-bit buffer offsets;
-// invalid lanes read out of range (hardware returns zero).
+// hash-grid encoding of the tile's 32 samples -> the two B fragments.
+//
+// Lane (c, h): sample c.  For every level the lane gathers the corners with
+// x bit = h of the 4 (y, z) rows, so ONE gather instruction covers the two
+// x-neighbours of a row for 32 samples: both sit in one 128-B line almost
+// always, and the cost of a gather instruction on gfx950 is its number of
+// distinct lines (measured: the same stream with every lane of an instruction
+// in one line runs as fast as with no memory access at all; tools/ablate.py
+// f1024).  28 lines/sample instead of 53 with one corner of two levels per
+// instruction (tools/atomic_sim.py's replay of the bench samples).
+// The two x-halves of each level are summed across the wave halves with
+// v_permlane32_swap (x0 half first, so both lanes hold the same value); each
+// lane keeps the 8 levels of its B-fragment rows (lane_level).
+// Gathers: 32-bit buffer offsets, 4 levels (16 loads) in flight per batch;
+// invalid lanes read out of range (zero, no memory access).
 __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
                                             __amdgpu_buffer_rsrc_t rs, int h, float ux, float uy,
                                             float uz, bool valid, half8& e0, half8& e1) {
     float f[16];
 #pragma unroll
-    for (int qb = 0; qb < 8; qb += 2) {
-        LevelPos P[2];
+    for (int lb = 0; lb < RN_L; lb += 4) {
+        LevelPos P[4];
         uint32_t off[16];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const LvConst lc = lv_const(T, a.gm, lane_level(qb + u, h));
+        for (int u = 0; u < 4; ++u) {
+            const LvConst lc = lv_const(T, a.gm, lb + u);
             P[u] = level_pos(lc.sc, ux, uy, uz);
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const uint32_t idx = corner_index(lc, P[u], c);
-                off[8 * u + c] = (valid && !(a.dbg & 128)) ? 4u * (lc.off + idx) : RN_OOB;
+            for (int r = 0; r < 4; ++r) {
+                const uint32_t idx = corner_index(lc, P[u], 2 * r + h);
+                const uint32_t ie = (a.dbg & 1024) ? (idx & 31u) : idx;   // ablation: 1 line per level
+                off[4 * u + r] = (valid && !(a.dbg & 128)) ? 4u * (lc.off + ie) : RN_OOB;
             }
         }
         uint32_t raw[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) raw[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i], 0, 0);
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < 4; ++u) {
             float a0 = 0.f, a1 = 0.f;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                const float w = corner_weight(P[u], c);
-                const uint32_t v = raw[8 * u + c];
-                const rn_half v0 = __builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu));
-                const rn_half v1 = __builtin_bit_cast(rn_half, (uint16_t)(v >> 16));
-                a0 = fmaf(w, (float)v0, a0);
-                a1 = fmaf(w, (float)v1, a1);
+            for (int r = 0; r < 4; ++r) {
+                const float w = corner_weight(P[u], 2 * r + h);
+                const uint32_t v = raw[4 * u + r];
+                a0 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu)), a0);
+                a1 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v >> 16)), a1);
             }
-            f[2 * (qb + u)] = a0; f[2 * (qb + u) + 1] = a1;
+            // x0 half (lanes 0-31) + x1 half (lanes 32-63), same order in both
+            const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false);
+            const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false);
+            const float v0 = __uint_as_float(s0[0]) + __uint_as_float(s0[1]);
+            const float v1 = __uint_as_float(s1[0]) + __uint_as_float(s1[1]);
+            // level L = lb + u belongs to the lanes with h == (L >> 1) & 1, at
+            // k-slot q = (L & 1) + 2 * (L >> 2)
+            const int L = lb + u, q = (L & 1) + 2 * (L >> 2);
+            if (((L >> 1) & 1) == h) { f[2 * q] = v0; f[2 * q + 1] = v1; }
         }
         // keep at most one batch of gathers in flight per wave: bounds VGPRs so
         // more waves fit (TLP hides the L2/MALL latency instead of ILP)

@@ -9,6 +9,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "radnerf.h"   // the C ABI: definitions below must match these declarations
 
 #pragma clang fp contract(off)
 
