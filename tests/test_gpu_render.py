@@ -1,0 +1,123 @@
+"""GPU: the remaining §8 rows end to end.
+
+  a11  single-NeRF `render()` with `NGP` (rendering.py:12-46, C1/C2): forward
+       and backward vs the CPU oracle (ml_oracle with K = 1, where the gate's
+       softmax over one model is exactly 1);
+  a10  test-time rendering (ml_rendering.py:81-155): with exp_step_factor 0 the
+       progressive-compaction loop must reproduce the training render with zero
+       jitter (same samples, same early termination);
+  §8f  density-grid maintenance (networks.py:375-409): the bitfield written by
+       update_density_grid equals packbits(density_grid > min(mean, thr)) of
+       the oracle on the updated grid, and the grid holds the field's σ at the
+       jittered cell positions.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import field_oracle as fo
+from oracle import ml_oracle
+from oracle.ml_oracle import _split_field
+from radnerf_amd import layout as LY
+from radnerf_amd import synthetic as S
+from radnerf_amd.networks import MNGP, NGP, Ray_Gate
+from radnerf_amd.rendering import ml_render, render
+
+pytestmark = pytest.mark.gpu
+
+
+def _init(m, K, p=0.5):
+    with torch.no_grad():
+        m.xyz_encoder.params.copy_(torch.from_numpy(S.grid_params(m.xyz_encoder.n_entries)).view(-1))
+        m.mlp_params.copy_(torch.from_numpy(S.mlp_params(K, LY.FIELD_PARAMS)))
+        bits = S.bitfields(K, m.cascades, p=p)
+        for i in range(K):
+            getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    return bits
+
+
+def test_ngp_render_train_vs_oracle(cuda):
+    scale, B = 0.5, 512
+    m = NGP(scale, seed=3)
+    bits = _init(m, 1)
+    m = m.to(cuda)
+    o, d = S.rays(B, scale)
+    nz = S.noise(1, B)
+    d_rgb, d_op, d_depth = S.loss_seeds(B, 1)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    res = render(m, t(o), t(d), noise=t(nz[0]))
+    torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
+                            [t(d_rgb), t(d_op), t(d_depth[:, 0])])
+    gate_p = np.zeros(LY.gate_params(1), np.float32)    # softmax over one model = 1
+    ref = ml_oracle.ml_train_step(o, d, bits, nz, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                  m.mlp_params.detach().cpu(), gate_p, scale,
+                                  seeds=(d_rgb, d_op, d_depth))
+    # bit-exact sample counts per ray
+    ra = res["rays_a"].cpu().numpy()
+    assert np.array_equal(ra[:, 2], ref["counts"][0])
+    e_rgb = np.abs(res["rgb"].detach().cpu().numpy() - ref["rgb"]).max()
+    e_op = np.abs(res["opacity"].detach().cpu().numpy() - ref["opacity"]).max()
+    e_de = np.abs(res["depth"].detach().cpu().numpy() - ref["depth"][:, 0]).max()
+    assert e_rgb <= 1e-4 and e_op <= 1e-4 and e_de <= 1e-4, (e_rgb, e_op, e_de)
+    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
+    assert rel(m.xyz_encoder.params.grad.cpu().view(-1, 2).numpy(), ref["grid_grad"]) <= 5e-2
+    assert rel(m.mlp_params.grad.cpu().numpy(), ref["mlp_grad"]) <= 5e-2
+
+
+@pytest.mark.parametrize("K", [1, 2])
+def test_test_time_render_matches_train_without_jitter(cuda, K):
+    scale, B = 0.5, 700
+    m = MNGP(scale, size=K, seed=3)
+    _init(m, K, p=0.3)
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6)[0]))
+    m, g = m.to(cuda), g.to(cuda)
+    o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, scale))
+    with torch.no_grad():
+        tr = ml_render(m, g, o, d, d, noise=torch.zeros(K, B, device=cuda))
+        te = ml_render(m, g, o, d, d, test_time=True)
+    for k in ("rgb", "opacity", "depth"):
+        err = (tr[k].float() - te[k].float()).abs().max().item()
+        assert err <= 1e-5, (k, err)
+
+
+def test_density_grid_update(cuda):
+    scale, K = 0.5, 2
+    m = MNGP(scale, size=K, seed=3)
+    _init(m, K)
+    m = m.to(cuda)
+    thr = 0.01 * 1024 / 3 ** 0.5                      # train_ml.py:175
+    with torch.no_grad():
+        for i in range(K):
+            getattr(m, f"density_grid_{i}").fill_(0.5)
+    torch.manual_seed(11)
+    m.update_density_grid(thr, warmup=True)
+    torch.cuda.synchronize()
+    # replay the update's random jitter (same generator, same call order)
+    torch.manual_seed(11)
+    gs = m.grid_size
+    coords = m.grid_coords
+    idx = oracle.morton3d(coords.cpu().numpy().astype(np.int32))
+    lv = fo.grid_levels(scale)
+    for i in range(K):
+        s = min(2 ** (0 - 1), scale)
+        half = s / gs
+        xw = (coords / (gs - 1) * 2 - 1) * (s - half)
+        xw = xw + (torch.rand_like(xw) * 2 - 1) * half
+        grid = getattr(m, f"density_grid_{i}").cpu().numpy()
+        # σ at a subset of cells vs the fp32 field oracle
+        sel = np.arange(0, len(idx), 997)
+        x_sel = xw[torch.from_numpy(sel).to(cuda)].cpu()
+        sig, _ = fo.field_forward(x_sel, torch.ones_like(x_sel),
+                                  m.xyz_encoder.params.detach().cpu().view(-1, 2).half().float(),
+                                  _split_field(m.mlp_params.detach().cpu()[i]), lv,
+                                  m.xyz_min.cpu(), m.xyz_max.cpu())
+        expect = np.maximum(0.5 * 0.95, sig.detach().numpy())
+        got = grid[0, idx[sel]]
+        assert np.allclose(got, expect, rtol=1e-2, atol=1e-6)
+        # bitfield == packbits(grid > min(mean, thr)) in Morton byte order
+        mean = grid[grid > 0].mean()
+        bits = oracle.packbits(grid.reshape(-1), min(float(mean), thr))
+        assert np.array_equal(getattr(m, f"density_bitfield_{i}").cpu().numpy(), bits)
