@@ -61,6 +61,9 @@ def parse():
                     help="rays in the bounded CPU-oracle sample: CPU baseline timing and the "
                          "rgb L_inf check (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
+                         "multi-rank path on one GPU")
     return ap.parse_args()
 
 
@@ -71,9 +74,10 @@ def main():
     from radnerf_amd.fused import FusedMLRenderer
     from radnerf_amd.networks import MNGP, Ray_Gate
 
-    rank, local, world = rdist.init()
+    rank, local, world = rdist.init(backend=None if args.backend == "auto" else args.backend)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    local = rdist.device_index(local)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     B, K, scale = args.rays, args.models, args.scale

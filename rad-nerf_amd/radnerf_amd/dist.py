@@ -19,6 +19,13 @@ def env_rank():
             int(os.environ.get("WORLD_SIZE", 1)))
 
 
+def device_index(local):
+    """GPU of this rank: LOCAL_RANK, unless RADNERF_DEVICE pins every rank to one
+    GPU (rehearsing the multi-rank path on a one-GPU box with gloo)."""
+    pinned = os.environ.get("RADNERF_DEVICE")
+    return int(pinned) if pinned is not None else local
+
+
 def init(backend=None):
     """Initialise the default process group from the torchrun env (no-op for 1 rank)."""
     rank, local, world = env_rank()
@@ -27,8 +34,9 @@ def init(backend=None):
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
-            torch.cuda.set_device(local)
-            dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            dev = device_index(local)
+            torch.cuda.set_device(dev)
+            dist.init_process_group(backend, device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(backend)
     return rank, local, world
