@@ -267,6 +267,25 @@ class MNGP(nn.Module):
                           density_bitfield)
             setattr(self, f"density_grid_{i}", density_grid)
 
+    @torch.no_grad()
+    def register_bbox(self, bbox):
+        """networks.py:413-422: scene box from a (2, 3) [min, max] array; resets
+        the cascades and every sub-NeRF's density grid / bitfield."""
+        bbox = np.asarray(bbox, dtype=np.float32)
+        dev = self.xyz_min.device
+        self.xyz_min = torch.from_numpy(bbox[0][None, :]).float().to(dev)
+        self.xyz_max = torch.from_numpy(bbox[1][None, :]).float().to(dev)
+        self.half_size = torch.from_numpy((bbox[1] - bbox[0]) / 2)[None, :].float().to(dev)
+        self.center = torch.from_numpy(np.mean(bbox, axis=0))[None, :].float().to(dev)
+        self.cascades = max(1 + int(np.ceil(np.log2(2 * float(self.half_size.max())))), 1)
+        for i in range(self.size):
+            setattr(self, f"density_bitfield_{i}",
+                    torch.zeros(self.cascades * self.grid_size ** 3 // 8, dtype=torch.uint8,
+                                device=dev))
+            setattr(self, f"density_grid_{i}",
+                    torch.zeros(self.cascades, self.grid_size ** 3, device=dev))
+        self._set_box_host()
+
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
         self._set_box_host()
