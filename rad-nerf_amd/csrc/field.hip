@@ -417,18 +417,21 @@ k_field_fwd(FieldArgs a) {
 //    27.2 with the hand-over.
 // ---------------------------------------------------------------------------
 #define SG_STRIDE 34
-#define SC_RING 128          // records per stream ring (power of two, >= 64 + 16)
+#define SC_STREAMS 8         // per wave: (quarter of the block's samples, level) pairs
+#define SC_RING 48           // entry records per stream ring (>= 31 pending + 2 steps x 8)
 
 // Finished runs are not issued by the lane that holds them: each of the
-// wave's 4 streams (half, level) compacts its finished runs (ballot + mbcnt)
-// into its own LDS ring of (byte offset, value) records and issues an atomic
-// instruction when 64 are pending, every lane active.  One instruction then
-// covers ~4-80 consecutive samples of ONE level of one ray, so entries of the
-// same 64-B segment that leave the cell at different steps (a ray moving
-// along x) share one request: 21.6 requests/sample (tools/atomic_sim.py).
+// wave's 8 streams (sample quarter, level) compacts its finished runs (ballot
+// + mbcnt) into its own LDS ring of (byte offset, f0, f1) entry records and
+// issues an atomic instruction when 32 entries (64 dwords) are pending, every
+// lane active.  One instruction then covers consecutive samples of ONE level
+// of one ray, so entries of the same 64-B segment that leave the cell at
+// different steps (a ray moving along x) share one request (tools/atomic_sim.py).
+// Ring storage is structure-of-arrays (offsets, f0, f1) so every LDS access
+// is a 4-B word.
 struct ScatterRing {
-    uint2* ring;             // this wave's 4 x SC_RING records
-    uint32_t head[4];        // per stream, wave-uniform
+    uint32_t* ring;          // this wave's SC_STREAMS x 3 x SC_RING words
+    uint32_t head[SC_STREAMS];   // per stream, wave-uniform (monotonic counters)
     uint32_t tail;           // per lane: the tail of this lane's stream
 };
 
@@ -436,92 +439,105 @@ __device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
     const int lane = rn_lane();
     asm volatile("" ::: "memory");
-    if ((uint32_t)lane < cnt) {
-        const uint2 r = R.ring[s * SC_RING + ((R.head[s] + lane) & (SC_RING - 1))];
-        if (dbg & 1) asm volatile("" :: "v"(r.x), "v"(r.y));
-        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(r.y), grad_rs,
-                                                             (int)r.x, 0, 0);
+    if ((uint32_t)lane < 2u * cnt) {
+        const uint32_t rec = (R.head[s] + (lane >> 1)) % SC_RING;
+        const uint32_t* base = R.ring + s * 3 * SC_RING;
+        const uint32_t off = base[rec] + 4u * (lane & 1);
+        const uint32_t v = base[(1 + (lane & 1)) * SC_RING + rec];
+        if (dbg & 1) asm volatile("" :: "v"(off), "v"(v));
+        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
+                                                             (int)off, 0, 0);
     }
     asm volatile("" ::: "memory");
     R.head[s] += cnt;
 }
 
 // append this step's finished runs (lanes with `emit`) to their stream rings;
-// no issue here (ring_drain runs every 4 steps: 63 pending + 4 x 16 <= 128)
+// no issue here (ring_drain runs every 2 steps: 31 pending + 2 x 8 < SC_RING)
 __device__ __forceinline__ void ring_push(ScatterRing& R, bool emit, uint64_t smask, uint32_t off,
-                                          float v) {
+                                          float v0, float v1) {
     const uint64_t m = __builtin_amdgcn_ballot_w64(emit) & smask;
     const uint32_t lo = (uint32_t)m, hi = (uint32_t)(m >> 32);
     const uint32_t rank = __builtin_amdgcn_mbcnt_hi(hi, __builtin_amdgcn_mbcnt_lo(lo, 0u));
-    const int s = rn_lane() >> 4;
-    if (emit)
-        R.ring[s * SC_RING + ((R.tail + rank) & (SC_RING - 1))] = make_uint2(off, __float_as_uint(v));
+    const int s = rn_lane() >> 3;
+    if (emit) {
+        uint32_t* base = R.ring + s * 3 * SC_RING;
+        const uint32_t rec = (R.tail + rank) % SC_RING;
+        base[rec] = off;
+        base[SC_RING + rec] = __float_as_uint(v0);
+        base[2 * SC_RING + rec] = __float_as_uint(v1);
+    }
     R.tail += (uint32_t)(__builtin_popcount(lo) + __builtin_popcount(hi));
 }
 
 __device__ __forceinline__ void ring_drain(ScatterRing& R, uint32_t min_cnt,
                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t t = __builtin_amdgcn_readlane(R.tail, 16 * q);
+    for (int q = 0; q < SC_STREAMS; ++q) {
+        const uint32_t t = __builtin_amdgcn_readlane(R.tail, 8 * q);
         const uint32_t pend = t - R.head[q];
-        if (pend >= min_cnt && pend > 0u) ring_issue(R, q, pend < 64u ? pend : 64u, grad_rs, dbg);
+        if (pend >= min_cnt && pend > 0u) ring_issue(R, q, pend < 32u ? pend : 32u, grad_rs, dbg);
     }
 }
 
+// Walk of one wave over the block's 256 samples.  Lane = (stream, corner):
+// stream = (quarter of the samples, level w or 15-w), one lane per corner
+// holding both features.  Each lane walks its 64 samples in ray order.
 __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvTab& sT,
                                                    const float* sG, const float* sU, int nblk,
                                                    ScatterRing& R,
                                                    __amdgpu_buffer_rsrc_t grad_rs) {
     const int lane = rn_lane();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-    const int half = lane >> 5, corner = (lane >> 1) & 7, feat = lane & 1;
+    const int stream = lane >> 3, quarter = stream >> 1, corner = lane & 7;
     const int cx = corner & 1, cy = (corner >> 1) & 1, cz = corner >> 2;
-    const int l = ((lane >> 4) & 1) ? (RN_L - 1 - wid) : wid;
+    const int l = (stream & 1) ? (RN_L - 1 - wid) : wid;
     const LvConst lc = lv_const(sT, a.gm, l);
-    const uint64_t smask = 0xffffull << (16 * (lane >> 4));
-    const int n0 = min(nblk, BWD_WAVES * 16);             // samples of half 0 (the longer)
-    const int nh = half ? nblk - n0 : n0;
-    const int s_base = half * (BWD_WAVES * 16);
-    const float* gcol = sG + 2 * l + feat;
+    const uint64_t smask = 0xffull << (8 * stream);
+    constexpr int QN = BWD_WAVES * 8;                     // samples per quarter
+    const int n0 = min(nblk, QN);                         // quarter 0 is the longest
+    const int nq = max(0, min(QN, nblk - quarter * QN));
+    const int s_base = quarter * QN;
+    const float* gcol = sG + 2 * l;
     int gx = -1000, gy = 0, gz = 0;                       // current cell (none yet)
     uint32_t cur = 0;
-    float acc = 0.f;
+    float acc0 = 0.f, acc1 = 0.f;
     // software pipeline: this step's sample row is loaded one step ahead
     float4 un = *reinterpret_cast<const float4*>(sU + s_base * 4);
-    float gn = gcol[s_base * SG_STRIDE];
-    for (int j0 = 0; j0 < n0; j0 += 4) {                  // wave-uniform trip count
+    float2 gn = *reinterpret_cast<const float2*>(gcol + s_base * SG_STRIDE);
+    for (int j0 = 0; j0 < n0; j0 += 2) {                  // wave-uniform trip count
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
+        for (int jj = 0; jj < 2; ++jj) {
             const int j = j0 + jj;
-            const bool act = j < nh;
+            const bool act = j < nq;
             const float4 uc = un;
-            const float gc = gn;
-            const int nx = s_base + (j + 1 < nh ? j + 1 : 0);
+            const float2 gc = gn;
+            const int nx = s_base + (j + 1 < nq ? j + 1 : 0);
             un = *reinterpret_cast<const float4*>(sU + nx * 4);
-            gn = gcol[nx * SG_STRIDE];
+            gn = *reinterpret_cast<const float2*>(gcol + nx * SG_STRIDE);
             const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
-            const float g = corner_weight(p, corner) * gc;
+            const float w = corner_weight(p, corner);
             const int dx = (int)p.gx - gx, dy = (int)p.gy - gy, dz = (int)p.gz - gz;
             // new corner c <- old corner c + delta (if that is a corner of the old cell)
             const int ox = cx + dx, oy = cy + dy, oz = cz + dz;
             const bool src_ok = (unsigned)ox <= 1u && (unsigned)oy <= 1u && (unsigned)oz <= 1u;
-            const int src = (lane & ~14) | ((src_ok ? ox + 2 * oy + 4 * oz : 0) << 1);
-            const float carried = __shfl(acc, src);
+            const int src = (lane & ~7) | (src_ok ? ox + 2 * oy + 4 * oz : 0);
+            const float c0 = __shfl(acc0, src), c1 = __shfl(acc1, src);
             // old corner c survives as new corner c - delta
             const int mx = cx - dx, my = cy - dy, mz = cz - dz;
             const bool keep = (unsigned)mx <= 1u && (unsigned)my <= 1u && (unsigned)mz <= 1u;
-            ring_push(R, act && !keep && gx != -1000, smask, 8u * (lc.off + cur) + 4u * feat, acc);
+            ring_push(R, act && !keep && gx != -1000, smask, 8u * (lc.off + cur), acc0, acc1);
             if (act) {
-                acc = (src_ok ? carried : 0.f) + g;
+                acc0 = (src_ok ? c0 : 0.f) + w * gc.x;
+                acc1 = (src_ok ? c1 : 0.f) + w * gc.y;
                 cur = corner_index(lc, p, corner);
                 gx = (int)p.gx; gy = (int)p.gy; gz = (int)p.gz;
             }
         }
-        ring_drain(R, 64u, grad_rs, a.dbg);
+        ring_drain(R, 32u, grad_rs, a.dbg);
     }
-    ring_push(R, gx != -1000, smask, 8u * (lc.off + cur) + 4u * feat, acc);
-    ring_drain(R, 64u, grad_rs, a.dbg);
+    ring_push(R, gx != -1000, smask, 8u * (lc.off + cur), acc0, acc1);
+    ring_drain(R, 32u, grad_rs, a.dbg);
 }
 
 // dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
@@ -559,7 +575,7 @@ k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[BWD_WAVES];
     __shared__ LvTab sT;
-    __shared__ uint2 sRing[BWD_WAVES * 4 * SC_RING];    // grid-gradient scatter rings
+    __shared__ uint32_t sRing[BWD_WAVES * SC_STREAMS * 3 * SC_RING];   // scatter rings
     const int k = blockIdx.y;
     rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                     FIELD_FRAGS * RN_FRAG_BYTES);
@@ -592,9 +608,9 @@ k_field_bwd(FieldArgs a) {
     static_assert(BWD_WAVES * 32 * (SG_STRIDE + 4) * 4 <= BWD_WAVES * 2 * RN_IMG_HALFS * 2,
                   "scatter staging must fit the image region");
     ScatterRing R;
-    R.ring = sRing + wid * 4 * SC_RING;
+    R.ring = sRing + wid * SC_STREAMS * 3 * SC_RING;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) R.head[q] = 0;
+    for (int q = 0; q < SC_STREAMS; ++q) R.head[q] = 0;
     R.tail = 0;
 
     for (int64_t it = blockIdx.x; it < n_iters; it += gridDim.x) {
