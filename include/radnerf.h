@@ -165,9 +165,8 @@ int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
                 int32_t n_models, const void* frags, float* gate, float* importance,
                 int32_t n_blocks, void* stream);
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
-                int32_t n_models, const void* frags, const int16_t* dw_map,
-                const float* dL_dgate, float* dw, int32_t n_params, int32_t n_blocks,
-                void* stream);
+                int32_t n_models, const void* frags, const float* dL_dgate, float* dw,
+                int32_t n_params, int32_t n_blocks, void* stream);
 
 /* ---- parameter packing (f32 master -> f16 MFMA fragments / f16 grid) ------*/
 int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,

@@ -18,7 +18,6 @@ struct GateArgs {
     int stride;
     int64_t n_rays; int K;
     const rn_half* frags;                        // [GATE_FRAGS][512]
-    const int16_t* dwmap;                        // [GATE_DW_TILES][16][64]
     float* gate;                                 // (B,K) softmax
     float* importance;                           // (K) gate.sum(0), may be null
     const float* dgate;                          // (B,K) dL/dgate
@@ -283,16 +282,16 @@ int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
 }
 
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays, int32_t n_models,
-                const void* frags, const int16_t* dw_map, const float* dL_dgate, float* dw,
-                int32_t n_params, int32_t n_blocks, void* stream) {
+                const void* frags, const float* dL_dgate, float* dw, int32_t n_params,
+                int32_t n_blocks, void* stream) {
     RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && n_models <= 16 && n_blocks >= 1, "bad sizes");
     RN_CHECK_ARG(n_params == 12672 + 64 * n_models, "n_params mismatch");
     if (n_rays == 0) return 0;
-    RN_CHECK_ARG(in0 && in1 && frags && dw_map && dL_dgate && dw && stride >= 3,
+    RN_CHECK_ARG(in0 && in1 && frags && dL_dgate && dw && stride >= 3,
                  "null pointer / bad stride");
     GateArgs a{};
     a.in0 = in0; a.in1 = in1; a.stride = stride; a.n_rays = n_rays; a.K = n_models;
-    a.frags = (const rn_half*)frags; a.dwmap = dw_map; a.dgate = dL_dgate; a.dw = dw;
+    a.frags = (const rn_half*)frags; a.dgate = dL_dgate; a.dw = dw;
     a.n_params = n_params;
     k_gate_bwd<<<n_blocks, GATE_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     RN_CHECK_LAUNCH();

@@ -213,10 +213,10 @@ class FusedMLRenderer:
         # gate backward beside field_bwd: it only needs dL/dgate (combine_bw)
         side = self._side(dev)
         main = torch.cuda.current_stream(dev)
-        frags, dwm = g.packed_frags(), g.dw_map(dev)
+        frags = g.packed_frags()
         side.wait_stream(main)
         self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
-                 frags.data_ptr(), dwm.data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
+                 frags.data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
                  gate_grad.numel(), max(1, min(128, (B + 127) // 128)), side.cuda_stream,
                  stream=side)
         self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)

@@ -178,9 +178,6 @@ class MNGP(nn.Module):
             self._frags_ver = p._version
         return self._frags
 
-    def dw_map(self, device):
-        return _DeviceTables.get("field_dw", device, LY.field_dw_map)
-
     def _launch_field(self, fwd, xyzs, dirs, ind, sigma=None, rgb=None, dsigma=None, drgb=None,
                       grid_grad=None, dw=None, blocks=None):
         dev = xyzs.device
@@ -348,8 +345,8 @@ class _GateFn(torch.autograd.Function):
             frags = g.packed_frags()
             nb = max(1, min(128, (B + 127) // 128))
             lib().gate_bwd(x.data_ptr(), x.data_ptr() + 12, 6, B, g.out_dim, frags.data_ptr(),
-                           g.dw_map(x.device).data_ptr(), dgate.float().contiguous().data_ptr(),
-                           dw.data_ptr(), dw.numel(), nb, _stream(x.device))
+                           dgate.float().contiguous().data_ptr(), dw.data_ptr(), dw.numel(), nb,
+                           _stream(x.device))
         return None, dw, None
 
 
@@ -383,10 +380,6 @@ class Ray_Gate(nn.Module):
                            self._frags.data_ptr(), _stream(p.device))
             self._frags_ver = p._version
         return self._frags
-
-    def dw_map(self, device):
-        return _DeviceTables.get(f"gate_dw_{self.out_dim}", device,
-                                 lambda: LY.gate_dw_map(self.out_dim))
 
     def forward(self, x, warmup=False):
         gate, _ = _GateFn.apply(x, self.params, self)
