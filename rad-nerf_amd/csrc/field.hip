@@ -640,6 +640,11 @@ k_field_bwd(FieldArgs a) {
         float bm = sMax[0];
 #pragma unroll
         for (int w = 1; w < BWD_WAVES; ++w) bm = fmaxf(bm, sMax[w]);
+        // an iteration whose 256 samples all have zero seeds (samples past the
+        // early-termination point of their rays, volumerendering.cu:150) adds
+        // nothing to the hash grid: its scatter walk is skipped (an early
+        // `continue` of the whole iteration made the compiler spill 190 B/lane)
+        const bool zero_iter = bm == 0.f;
         const float gscale = rn_wave_grad_scale(bm);   // uniform over the block
         if (cur_scale != gscale) {                     // exact power-of-two rescale
             const float r = cur_scale == 0.f ? 0.f : gscale / cur_scale;
@@ -737,7 +742,7 @@ k_field_bwd(FieldArgs a) {
         __syncthreads();                                                    // B10
 
         // ---- hash-grid gradient scatter (grid_scatter_block)
-        if (do_sc) {
+        if (do_sc && !zero_iter) {
             const float ginv = 1.0f / gscale;
             const int srow = wid * 32 + c;
 #pragma unroll

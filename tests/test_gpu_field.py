@@ -63,7 +63,11 @@ def test_field_forward(cuda, scale):
         assert e_sig.max() <= 1e-2, e_sig.max()
 
 
-def test_field_backward(cuda):
+@pytest.mark.parametrize("zero_span", [None, (600, 3100)])
+def test_field_backward(cuda, zero_span):
+    """zero_span: samples whose seeds are zero (as past a ray's early
+    termination); covers whole 256-sample backward iterations, which the
+    kernel skips, and partial ones."""
     scale = 0.5
     m = _model(cuda, scale)
     n = 4000
@@ -71,6 +75,9 @@ def test_field_backward(cuda):
     rng = np.random.default_rng(8)
     ds = rng.normal(0, 1, n).astype(np.float32)
     dr = rng.normal(0, 1, (n, 3)).astype(np.float32)
+    if zero_span is not None:
+        ds[zero_span[0]:zero_span[1]] = 0
+        dr[zero_span[0]:zero_span[1]] = 0
     ind = 1
     m.zero_grad()
     sig, rgb = m(torch.from_numpy(x).to(cuda), torch.from_numpy(d).to(cuda), ind)
