@@ -49,10 +49,10 @@ def _run(fn, m, g, o, d, noise, seeds, cuda, esf):
     return res, grads
 
 
-@pytest.mark.parametrize("scale", [0.5, 16.0])
-def test_fused_vs_dropin_vs_oracle(cuda, scale):
+@pytest.mark.parametrize("scale,K", [(0.5, 2), (16.0, 2), (0.5, 4)])
+def test_fused_vs_dropin_vs_oracle(cuda, scale, K):
     esf = 1 / 256 if scale > 0.5 else 0.0
-    m, g, o, d, noise, seeds, bits = _setup(cuda, scale=scale)
+    m, g, o, d, noise, seeds, bits = _setup(cuda, scale=scale, K=K)
     rf, gf = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     rd, gd = _run(ml_render, m, g, o, d, noise, seeds, cuda, esf)
     for k in ("rgb", "opacity", "depth", "gating_code"):

@@ -63,12 +63,19 @@ def _near_clamp(ht):
     return ht
 
 
-@pytest.mark.parametrize("scale,p", [(0.5, 0.5), (0.5, 0.1), (16.0, 0.5), (0.5, 1.0), (0.5, 0.0)])
-def test_raymarching_train_bit_exact(cuda, scale, p):
+@pytest.mark.parametrize("scale,p,esf,max_samples", [
+    (0.5, 0.5, None, 1024), (0.5, 0.1, None, 1024), (16.0, 0.5, None, 1024),
+    (0.5, 1.0, None, 1024), (0.5, 0.0, None, 1024),
+    # full grid, constant dt, box diagonal 3.5: rays hit the 1024-sample cap
+    (1.0, 1.0, 0.0, 1024),
+    # a cap that falls inside a 64-step chunk of the wave march
+    (1.0, 0.7, 0.0, 100)])
+def test_raymarching_train_bit_exact(cuda, scale, p, esf, max_samples):
     n = 2048
     o, d = S.rays(n, scale)
     cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)
-    esf = 1 / 256 if scale > 0.5 else 0.0
+    if esf is None:
+        esf = 1 / 256 if scale > 0.5 else 0.0
     bits = S.bitfields(1, cascades, p=p)[0]
     nz = S.noise(1, n)[0]
     _, ht, _, _, oht, _ = _hits(o, d, scale, cuda)
@@ -76,9 +83,9 @@ def test_raymarching_train_bit_exact(cuda, scale, p):
     h2 = np.ascontiguousarray(ht_np[:, 0])
     rays_a, xyzs, dirs, deltas, ts, counter = vren.raymarching_train(
         _t(o, cuda), _t(d, cuda), _t(h2, cuda), _t(bits, cuda), cascades, scale, esf,
-        _t(nz, cuda), 128, 1024)
+        _t(nz, cuda), 128, max_samples)
     ora, oxyz, odir, odl, ots, otot = oracle.raymarching_train(o, d, h2, bits, cascades, scale,
-                                                               esf, nz, 128, 1024)
+                                                               esf, nz, 128, max_samples)
     assert int(counter[0]) == otot and int(counter[1]) == n
     assert np.array_equal(rays_a.cpu().numpy(), ora)
     for a, b in ((xyzs, oxyz), (dirs, odir), (deltas, odl), (ts, ots)):
@@ -86,7 +93,9 @@ def test_raymarching_train_bit_exact(cuda, scale, p):
     if p == 0.0:
         assert otot == 0
     if p == 1.0:
-        assert ora[:, 2].max() <= 1024 and otot > 0
+        assert ora[:, 2].max() <= max_samples and otot > 0
+    if esf == 0.0 and scale == 1.0:
+        assert ora[:, 2].max() == max_samples       # the cap is exercised
 
 
 def test_raymarching_test_bit_exact(cuda):
