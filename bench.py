@@ -61,6 +61,8 @@ def parse():
                     help="rays in the bounded CPU-oracle sample: CPU baseline timing and the "
                          "rgb L_inf check (0 = skip)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
+    ap.add_argument("--train-step", type=int, default=1,
+                    help="also time the full train step (loss + Adam); 0 = skip")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
                          "multi-rank path on one GPU")
@@ -148,6 +150,47 @@ def main():
         dist.all_reduce(fwd_elapsed, op=dist.ReduceOp.MAX)
     fwd_only = {"value": round(int(fwd_acc) / float(fwd_elapsed) / 1e6, 2), "unit": "Msamples/s",
                 "ms_per_step": round(float(fwd_elapsed) / args.steps * 1e3, 4)}
+
+    # full training step of train_ml.py: render ->
+    # fused NeRFLoss (opacity 1e-3, CV^2 1e-2, depth-mutual 5e-2) -> backward ->
+    # (all-reduce) -> FusedAdam; synthetic target colours.  Not part of `value`.
+    train = None
+    if args.train_step:
+        from radnerf_amd.optim import FusedAdam
+        params = [model.xyz_encoder.params, model.mlp_params, gate.params]
+        for p_, v_ in zip(params, ar.views):
+            p_.grad = v_
+        opt = FusedAdam(params, lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+        tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(7 + rank)).to(dev)
+
+        def tstep(i):
+            ar.zero()
+            r.train_step(rays_o, rays_d, rays_d, tgt, noises[i % 4], bg, 1e-3, 1e-2, 5e-2,
+                         1e-4, esf, ar.views[0], ar.views[1], ar.views[2])
+            if world > 1:
+                ar.reduce()
+            opt.step()
+
+        for i in range(2):
+            tstep(i)
+        tr_acc = torch.zeros((), dtype=torch.int64, device=dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            tstep(i)
+            tr_acc.add_(r.ws.meta[1])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        tr_el = torch.tensor(time.perf_counter() - t0, device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(tr_acc)
+            dist.all_reduce(tr_el, op=dist.ReduceOp.MAX)
+        train = {"value": round(int(tr_acc) / float(tr_el) / 1e6, 2), "unit": "Msamples/s",
+                 "ms_per_step": round(float(tr_el) / args.steps * 1e3, 4),
+                 "includes": "render + fused loss + backward + FusedAdam"}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:
@@ -211,6 +254,7 @@ def main():
                "roofline": roofline, "cpu_baseline": cpu_base,
                "rgb_linf_vs_ref": rgb_linf,
                "forward_only": fwd_only,
+               "train_step": train,
                # MFMA use: algorithmic MLP flops (56,832 per sample
                # fwd+bwd, unpadded) at `value`, against the dense f16 peak
                "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),

@@ -168,6 +168,25 @@ int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
                 int32_t n_models, const void* frags, const float* dL_dgate, float* dw,
                 int32_t n_params, int32_t n_blocks, void* stream);
 
+/* ---- training-step epilogue ---------------------
+ * rn_nerf_loss: losses.py:44-76 (NeRFLoss: rgb MSE, opacity entropy, CV^2 of
+ * the gate importance, depth-mutual) fused with its backward.  Inputs are the
+ * ml_render outputs rgb (B,3), opacity (B), depth (B,K), gating_code (B,K),
+ * gating_importance (K).  loss_out[4] = sums of the four terms (lambdas
+ * applied; [0] over B*3, [1] over B, [2] the CV^2 scalar, [3] over B*K):
+ * divide by the element counts for the reference's per-term means.  Seeds:
+ * the gradients of sum(term.mean()) w.r.t. rgb, opacity, depth and gate.
+ * rn_adam: torch.optim.Adam step (train_ml.py:138-153, apex FusedAdam with
+ * eps 1e-15) over n fp32 params; optional f16 mirror of params[0, n_f16).   */
+int rn_nerf_loss(const float* rgb, const float* target_rgb, const float* opacity,
+                 const float* depth, const float* gate, const float* importance, int64_t n_rays,
+                 int32_t n_models, float lambda_opacity, float lambda_cv, float lambda_dm,
+                 float* loss_out, float* dL_drgb, float* dL_dopacity, float* dL_ddepth,
+                 float* dL_dgate, void* stream);
+int rn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+            float lr, float beta1, float beta2, float eps, int32_t step, float grad_scale,
+            void* params_f16, int64_t n_f16, void* stream);
+
 /* ---- parameter packing (f32 master -> f16 MFMA fragments / f16 grid) ------*/
 int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,
                 int32_t n_models, int64_t dst_stride, void* dst, void* stream);

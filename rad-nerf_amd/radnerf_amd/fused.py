@@ -225,6 +225,25 @@ class FusedMLRenderer:
         return grid_grad, mlp_grad, gate_grad
 
 
+    # --------------------------------------------------------------- train step
+    def train_step(self, rays_o, rays_d, gate_in2, target_rgb, noise, bg, lambda_opacity=1e-3,
+                   lambda_cv_importance=0.0, lambda_depth_mutual=0.0, T_threshold=1e-4,
+                   exp_step_factor=0.0, grid_grad=None, mlp_grad=None, gate_grad=None):
+        """render -> NeRFLoss -> backward of train_ml.py:179-192 as one launch
+        chain: the fused loss kernel writes the backward seeds directly.
+        Returns ({term: mean}, (grid_grad, mlp_grad, gate_grad)); gradients are
+        accumulated into the given buffers (zero them first)."""
+        from .losses import fused_nerf_loss
+        rgb, opacity, depth, gate, imp = self.forward(rays_o, rays_d, gate_in2, noise, bg,
+                                                      T_threshold, exp_step_factor)
+        terms, (d_rgb, d_op, d_depth, d_gate) = fused_nerf_loss(
+            rgb, target_rgb, opacity, depth, gate, imp, lambda_opacity, lambda_cv_importance,
+            lambda_depth_mutual)
+        grads = self.backward(rays_o, rays_d, gate_in2, gate, bg, d_rgb, d_op, d_depth, d_gate,
+                              T_threshold, grid_grad, mlp_grad, gate_grad)
+        return terms, grads
+
+
 class _MLRenderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, grid_params, mlp_params, gate_params, renderer, rays_o, rays_d, gate_in2,

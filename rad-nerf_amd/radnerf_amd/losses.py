@@ -1,0 +1,67 @@
+"""NeRFLoss of the reference (losses.py:39-76) in two forms.
+
+`NeRFLoss`         the reference module: a dict of loss tensors built from torch
+                   ops (autograd), for callers that keep the reference training
+                   loop (`loss = sum(l.mean() for l in loss_d.values())`).
+`fused_nerf_loss`  one HIP pass (rn_nerf_loss) that returns the per-term means
+                   AND the seeds dL/drgb, dL/dopacity, dL/ddepth, dL/dgate of
+                   `sum(term.mean())`; FusedMLRenderer.train_step feeds them
+                   straight into the fused backward (no autograd graph).
+
+The distortion (vren.distortion_loss_*) and disparity terms default to 0 in
+train_ml.py and are out of scope.
+"""
+import torch
+from torch import nn
+
+from ._lib import lib
+
+
+class NeRFLoss(nn.Module):
+    """losses.py:39-76 (without the distortion / disparity terms)."""
+
+    def __init__(self, lambda_opacity=1e-3):
+        super().__init__()
+
+    def forward(self, results, target, lambda_opacity=1e-3, lambda_distortion=0, lambda_disp=0,
+                lambda_cv_importance=0, lambda_depth_mutual=0):
+        if lambda_distortion > 0 or lambda_disp > 0:
+            raise NotImplementedError("distortion / disparity losses are out of scope")
+        loss = {}
+        loss["rgb"] = (results["rgb"] - target["rgb"]) ** 2
+        o = results["opacity"] + 1e-10
+        loss["opacity"] = lambda_opacity * (-o * torch.log(o))
+        K = results["gating_code"].shape[-1]
+        if lambda_cv_importance > 0 and K > 1:
+            imp = results["gating_importance"].float()
+            loss["cv_importance"] = lambda_cv_importance * imp.var() / (imp.mean() ** 2 + 1e-10)
+        if lambda_depth_mutual > 0 and K > 1:
+            d = results["depth"]
+            loss["depth_mutual"] = lambda_depth_mutual * (
+                (d - torch.sum(d * results["gating_code"], 1, keepdim=True).detach()) ** 2)
+        return loss
+
+
+def fused_nerf_loss(rgb, target_rgb, opacity, depth, gate, importance, lambda_opacity=1e-3,
+                    lambda_cv_importance=0.0, lambda_depth_mutual=0.0):
+    """Returns ({term: mean (0-d tensor)}, (dL_drgb, dL_dopacity, dL_ddepth, dL_dgate))
+    for loss = sum of the term means.  All inputs fp32 CUDA, contiguous."""
+    B, K = gate.shape
+    dev = rgb.device
+    f = lambda *s: torch.empty(*s, device=dev, dtype=torch.float32)
+    out = f(4)
+    d_rgb, d_op, d_depth, d_gate = f(B, 3), f(B), f(B, K), f(B, K)
+    c = lambda t: t.float().contiguous()
+    rgb, target_rgb, opacity, depth, gate, importance = map(
+        c, (rgb, target_rgb, opacity, depth, gate, importance))
+    lib().nerf_loss(rgb.data_ptr(), target_rgb.data_ptr(), opacity.data_ptr(), depth.data_ptr(),
+                    gate.data_ptr(), importance.data_ptr(), B, K, float(lambda_opacity),
+                    float(lambda_cv_importance), float(lambda_depth_mutual), out.data_ptr(),
+                    d_rgb.data_ptr(), d_op.data_ptr(), d_depth.data_ptr(), d_gate.data_ptr(),
+                    torch.cuda.current_stream(dev).cuda_stream)
+    terms = {"rgb": out[0] / (3 * B), "opacity": out[1] / B}
+    if lambda_cv_importance > 0 and K > 1:
+        terms["cv_importance"] = out[2]
+    if lambda_depth_mutual > 0 and K > 1:
+        terms["depth_mutual"] = out[3] / (B * K)
+    return terms, (d_rgb, d_op, d_depth, d_gate)

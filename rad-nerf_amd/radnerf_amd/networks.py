@@ -79,14 +79,25 @@ class HashGridEncoding(nn.Module):
 
     def params_f16(self):
         """f16 copy of the table (tcnn keeps the table in f16), refreshed when
-        the fp32 master changes."""
+        the fp32 master changes.  radnerf_amd.optim.FusedAdam refreshes it in
+        its own pass and marks it current (p._rn_f16_key)."""
         p = self.params
-        if self._f16 is None or self._f16.device != p.device or self._f16_ver != p._version:
+        key = _param_key(p)
+        if self._f16 is not None and getattr(p, "_rn_f16_key", None) == key:
+            self._f16_ver = key
+        if self._f16 is None or self._f16.device != p.device or self._f16_ver != key:
             if self._f16 is None or self._f16.device != p.device:
                 self._f16 = torch.empty(p.numel(), dtype=torch.float16, device=p.device)
+                p._rn_f16 = self._f16
             lib().to_f16(p.data_ptr(), p.numel(), self._f16.data_ptr(), _stream(p.device))
-            self._f16_ver = p._version
+            self._f16_ver = key
         return self._f16
+
+
+def _param_key(p):
+    """Version key of a parameter's derived caches: torch's in-place version
+    plus the epoch radnerf_amd.optim.FusedAdam bumps after its kernel update."""
+    return (p._version, getattr(p, "_rn_epoch", 0))
 
 
 class _FieldFn(torch.autograd.Function):
@@ -168,14 +179,14 @@ class MNGP(nn.Module):
     def packed_frags(self):
         """f16 MFMA fragments of all sub-NeRFs, (size, 46*512) halfs."""
         p = self.mlp_params
-        if self._frags is None or self._frags.device != p.device or self._frags_ver != p._version:
+        if self._frags is None or self._frags.device != p.device or self._frags_ver != _param_key(p):
             idx = _DeviceTables.get("field_frags", p.device, LY.field_frag_index)
             if self._frags is None or self._frags.device != p.device:
                 self._frags = torch.empty(self.size, idx.numel(), dtype=torch.float16,
                                           device=p.device)
             lib().pack_f16(p.data_ptr(), LY.FIELD_PARAMS, idx.data_ptr(), idx.numel(), self.size,
                            idx.numel(), self._frags.data_ptr(), _stream(p.device))
-            self._frags_ver = p._version
+            self._frags_ver = _param_key(p)
         return self._frags
 
     def _launch_field(self, fwd, xyzs, dirs, ind, sigma=None, rgb=None, dsigma=None, drgb=None,
@@ -371,14 +382,14 @@ class Ray_Gate(nn.Module):
 
     def packed_frags(self):
         p = self.params
-        if self._frags is None or self._frags.device != p.device or self._frags_ver != p._version:
+        if self._frags is None or self._frags.device != p.device or self._frags_ver != _param_key(p):
             idx = _DeviceTables.get(f"gate_frags_{self.out_dim}", p.device,
                                     lambda: LY.gate_frag_index(self.out_dim))
             if self._frags is None or self._frags.device != p.device:
                 self._frags = torch.empty(idx.numel(), dtype=torch.float16, device=p.device)
             lib().pack_f16(p.data_ptr(), p.numel(), idx.data_ptr(), idx.numel(), 1, idx.numel(),
                            self._frags.data_ptr(), _stream(p.device))
-            self._frags_ver = p._version
+            self._frags_ver = _param_key(p)
         return self._frags
 
     def forward(self, x, warmup=False):

@@ -1,0 +1,50 @@
+"""Adam step on the HIP library.
+
+Replaces apex.FusedAdam(lr, eps=1e-15) of train_ml.py:138-153 (apex is not
+available on ROCm as-is): torch.optim.Adam semantics without weight decay, one
+pass per parameter tensor (rn_adam).  For the hash table the same pass writes
+the f16 copy the field kernels gather from, so the next step does not need a
+separate conversion.
+"""
+import torch
+
+from ._lib import lib
+
+
+class FusedAdam(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-2, betas=(0.9, 0.99), eps=1e-15, weight_decay=0.0):
+        if weight_decay != 0.0:
+            raise NotImplementedError("weight decay: train_ml.py uses none")
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+
+    @torch.no_grad()
+    def step(self, closure=None, grad_scale=1.0):
+        loss = closure() if closure is not None else None
+        for group in self.param_groups:
+            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+                    raise RuntimeError("FusedAdam: fp32 contiguous CUDA parameters only")
+                st = self.state[p]
+                if not st:
+                    st["step"] = 0
+                    st["exp_avg"] = torch.zeros_like(p)
+                    st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] += 1
+                g = p.grad.contiguous()
+                mirror = getattr(p, "_rn_f16", None)     # f16 copy kept by HashGridEncoding
+                lib().adam(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                           st["exp_avg_sq"].data_ptr(), p.numel(), float(group["lr"]), float(b1),
+                           float(b2), float(group["eps"]), int(st["step"]), float(grad_scale),
+                           None if mirror is None else mirror.data_ptr(),
+                           0 if mirror is None else p.numel(),
+                           torch.cuda.current_stream(p.device).cuda_stream)
+                # the kernel wrote p in place behind autograd's back: bump the
+                # epoch the modules' derived caches (f16 fragments) key on; the
+                # f16 table mirror was refreshed by the same pass
+                p._rn_epoch = getattr(p, "_rn_epoch", 0) + 1
+                if mirror is not None:
+                    p._rn_f16_key = (p._version, p._rn_epoch)
+        return loss

@@ -1,0 +1,131 @@
+"""GPU: §8(f) rows 2-3 -- the fused NeRFLoss (rn_nerf_loss) and the Adam step
+(rn_adam) against the reference formulas evaluated with torch autograd / torch
+optimizers on the same inputs, and the fused train step (render -> loss ->
+backward) against autograd through ml_render_fused + the reference loss."""
+import numpy as np
+import pytest
+import torch
+
+from radnerf_amd import layout as LY
+from radnerf_amd import synthetic as S
+from radnerf_amd.fused import get_renderer, ml_render_fused
+from radnerf_amd.losses import NeRFLoss, fused_nerf_loss
+from radnerf_amd.networks import MNGP, Ray_Gate
+from radnerf_amd.optim import FusedAdam
+
+pytestmark = pytest.mark.gpu
+
+LAMBDAS = dict(lambda_opacity=1e-3, lambda_cv_importance=1e-2, lambda_depth_mutual=5e-2)
+
+
+def _results(cuda, B, K, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    gate = torch.softmax(torch.randn(B, K, generator=g), 1)
+    res = {"rgb": torch.rand(B, 3, generator=g), "opacity": torch.rand(B, generator=g),
+           "depth": torch.rand(B, K, generator=g) * 3, "gating_code": gate,
+           "gating_importance": gate.sum(0)}
+    target = {"rgb": torch.rand(B, 3, generator=g)}
+    return res, target
+
+
+@pytest.mark.parametrize("K", [1, 2, 4])
+def test_fused_loss_matches_reference_formula(cuda, K):
+    B = 3000
+    res, target = _results(cuda, B, K)
+    # reference: losses.py NeRFLoss + train_ml.py sum of means, autograd on CPU fp64
+    leaves = {k: v.double().requires_grad_(True) for k, v in res.items() if k != "gating_importance"}
+    leaves_res = dict(leaves, gating_importance=leaves["gating_code"].sum(0))
+    ld = NeRFLoss()(leaves_res, {"rgb": target["rgb"].double()}, **LAMBDAS)
+    total = sum(v.mean() for v in ld.values())
+    total.backward()
+    c = lambda t: t.to(cuda)
+    terms, (d_rgb, d_op, d_depth, d_gate) = fused_nerf_loss(
+        c(res["rgb"]), c(target["rgb"]), c(res["opacity"]), c(res["depth"]),
+        c(res["gating_code"]), c(res["gating_importance"]), **LAMBDAS)
+    assert set(terms) == set(ld)
+    for k in ld:
+        assert abs(float(terms[k]) - float(ld[k].mean().detach())) <= 1e-5 * max(1.0, abs(float(ld[k].mean().detach()))), k
+    def close(a, b):
+        b = torch.zeros(a.shape, dtype=torch.float64) if b is None else b   # term absent
+        return torch.allclose(a.cpu().double(), b, rtol=1e-4, atol=1e-9)
+    assert close(d_rgb, leaves["rgb"].grad)
+    assert close(d_op, leaves["opacity"].grad)
+    assert close(d_depth, leaves["depth"].grad)
+    # the reference's gate gradient from the loss: CV^2 through gating_importance
+    # and the (detached) depth-mutual mean contributes nothing
+    assert close(d_gate, leaves["gating_code"].grad)
+
+
+def test_fused_adam_matches_torch_adam(cuda):
+    g = torch.Generator().manual_seed(3)
+    p0 = torch.randn(100_003, generator=g)
+    grads = [torch.randn(100_003, generator=g) * 1e-2 for _ in range(5)]
+    ref = torch.nn.Parameter(p0.clone())
+    opt_ref = torch.optim.Adam([ref], lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    ours = torch.nn.Parameter(p0.clone().to(cuda))
+    opt = FusedAdam([ours], lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    for gr in grads:
+        ref.grad = gr.clone()
+        opt_ref.step()
+        ours.grad = gr.to(cuda)
+        opt.step()
+    assert torch.allclose(ours.detach().cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    st, st_ref = opt.state[ours], opt_ref.state[ref]
+    assert torch.allclose(st["exp_avg"].cpu(), st_ref["exp_avg"], rtol=1e-5, atol=1e-9)
+    assert torch.allclose(st["exp_avg_sq"].cpu(), st_ref["exp_avg_sq"], rtol=1e-5, atol=1e-12)
+
+
+def _setup(cuda, B, K, scale=0.5):
+    m = MNGP(scale, size=K, seed=3)
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        m.xyz_encoder.params.copy_(torch.from_numpy(S.grid_params(m.xyz_encoder.n_entries)).view(-1))
+        m.mlp_params.copy_(torch.from_numpy(S.mlp_params(K, LY.FIELD_PARAMS)))
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6)[0]))
+        bits = S.bitfields(K, m.cascades, p=0.5)
+        for i in range(K):
+            getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    return m.to(cuda), g.to(cuda)
+
+
+def test_fused_train_step_matches_autograd(cuda):
+    B, K = 512, 2
+    m, g = _setup(cuda, B, K)
+    o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, 0.5))
+    nz = torch.from_numpy(S.noise(K, B)).to(cuda)
+    tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(5)).to(cuda)
+    # reference structure: render (autograd) -> NeRFLoss -> sum of means -> backward
+    m.zero_grad(); g.zero_grad()
+    res = ml_render_fused(m, g, o, d, d, noise=nz)
+    ld = NeRFLoss()(res, {"rgb": tgt}, **LAMBDAS)
+    sum(v.mean() for v in ld.values()).backward()
+    ref = [m.xyz_encoder.params.grad.clone(), m.mlp_params.grad.clone(), g.params.grad.clone()]
+    # fused train step
+    r = get_renderer(m, g, B)
+    bg = torch.ones(3, device=cuda)
+    terms, grads = r.train_step(o, d, d, tgt, nz, bg, **LAMBDAS)
+    for k in ld:
+        assert abs(float(terms[k]) - float(ld[k].mean().detach())) <= 1e-5 * max(1.0, abs(float(ld[k].mean().detach()))), k
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))
+    for a, b in zip(grads, ref):
+        assert rel(a, b) <= 1e-3, rel(a, b)
+
+
+def test_adam_refreshes_derived_caches(cuda):
+    """After an in-place kernel update the f16 table mirror is current and the
+    MLP fragments are repacked (no stale weights in the next forward)."""
+    B, K = 256, 2
+    m, g = _setup(cuda, B, K)
+    o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, 0.5))
+    nz = torch.from_numpy(S.noise(K, B)).to(cuda)
+    ml_render_fused(m, g, o, d, d, noise=nz)                    # builds the caches
+    opt = FusedAdam([m.xyz_encoder.params, m.mlp_params, g.params], lr=1e-2)
+    for p in (m.xyz_encoder.params, m.mlp_params, g.params):
+        p.grad = torch.randn_like(p) * 1e-3
+    opt.step()
+    f16 = m.xyz_encoder.params_f16()
+    assert torch.equal(f16, m.xyz_encoder.params.detach().half())
+    frags = m.packed_frags().clone()
+    with torch.no_grad():
+        m.mlp_params.add_(0)                                      # forces a fresh repack
+    assert torch.equal(m.packed_frags(), frags)
