@@ -187,6 +187,14 @@ int rn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq
             float lr, float beta1, float beta2, float eps, int32_t step, float grad_scale,
             void* params_f16, int64_t n_f16, void* stream);
 
+/* rn_get_rays: train_ml.py:84-96 + ray_utils.py:45-70 for a batch of picks.
+ * directions (P,3) camera-space; poses (I,3,4) c2w; img_idxs (n) or NULL
+ * (one pose); pix_idxs (n) or NULL (directions are per ray).  imgs_d (n,3)
+ * (the gate's 'image' input: the pose applied to mean_dir) may be NULL.      */
+int rn_get_rays(const float* directions, const float* poses, const int64_t* img_idxs,
+                const int64_t* pix_idxs, int64_t n_rays, const float* mean_dir, float* rays_o,
+                float* rays_d, float* imgs_d, void* stream);
+
 /* ---- parameter packing (f32 master -> f16 MFMA fragments / f16 grid) ------*/
 int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,
                 int32_t n_models, int64_t dst_stride, void* dst, void* stream);

@@ -120,6 +120,28 @@ k_adam(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __r
     }
 }
 
+// train_ml.py:84-96 + datasets/ray_utils.py:45-70 (get_rays) for a batch of
+// (image, pixel) picks: rays_d = R dir, rays_o = T, imgs_d = R mean_dir.
+// The 3x3 rotation is applied as three dot products in (x, y, z) order.
+__global__ void __launch_bounds__(256)
+k_get_rays(int64_t n, const float* __restrict__ dirs, const float* __restrict__ poses,
+           const int64_t* __restrict__ img_idx, const int64_t* __restrict__ pix_idx,
+           const float* __restrict__ mean_dir, float* __restrict__ rays_o,
+           float* __restrict__ rays_d, float* __restrict__ imgs_d) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n) return;
+    const float* P = poses + 12 * (img_idx ? img_idx[r] : 0);     // (3, 4) row-major
+    const float* d = dirs + 3 * (pix_idx ? pix_idx[r] : r);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        rays_d[3 * r + i] = d[0] * P[4 * i] + d[1] * P[4 * i + 1] + d[2] * P[4 * i + 2];
+        rays_o[3 * r + i] = P[4 * i + 3];
+        if (imgs_d)
+            imgs_d[3 * r + i] = mean_dir[0] * P[4 * i] + mean_dir[1] * P[4 * i + 1] +
+                                mean_dir[2] * P[4 * i + 2];
+    }
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -159,6 +181,18 @@ int rn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq
     k_adam<<<blocks, 256, 0, (hipStream_t)stream>>>(n, params, grads, exp_avg, exp_avg_sq, lr,
                                                     beta1, beta2, eps, bc1, bc2, grad_scale,
                                                     (_Float16*)params_f16, n_f16);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_get_rays(const float* directions, const float* poses, const int64_t* img_idxs,
+                const int64_t* pix_idxs, int64_t n_rays, const float* mean_dir, float* rays_o,
+                float* rays_d, float* imgs_d, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(directions && poses && rays_o && rays_d && (!imgs_d || mean_dir), "null pointer");
+    k_get_rays<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+        n_rays, directions, poses, img_idxs, pix_idxs, mean_dir, rays_o, rays_d, imgs_d);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -44,6 +44,7 @@ SIGNATURES = {
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],
     "rn_adam": [P, P, P, P, I64, F32, F32, F32, F32, I32, F32, P, I64, P],
+    "rn_get_rays": [P, P, P, P, I64, P, P, P, P, P],
     "rn_pack_f16": [P, I64, P, I64, I32, I64, P, P],
     "rn_to_f16": [P, I64, P, P],
     "rn_morton3d": [P, I64, P, P],

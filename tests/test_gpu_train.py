@@ -129,3 +129,27 @@ def test_adam_refreshes_derived_caches(cuda):
     with torch.no_grad():
         m.mlp_params.add_(0)                                      # forces a fresh repack
     assert torch.equal(m.packed_frags(), frags)
+
+
+def test_batch_rays_match_reference_formula(cuda):
+    """train_ml.py:84-96 / ray_utils.py:45-70 restated in torch (CPU fp64)."""
+    from radnerf_amd.rays import batch_rays, get_rays
+    g = torch.Generator().manual_seed(9)
+    H, W, n_img, n = 40, 50, 7, 4096
+    dirs = torch.stack([torch.rand(H * W, generator=g) - 0.5, torch.rand(H * W, generator=g) - 0.5,
+                        torch.ones(H * W)], -1)
+    q, _ = torch.linalg.qr(torch.randn(n_img, 3, 3, generator=g))
+    poses = torch.cat([q, torch.randn(n_img, 3, 1, generator=g)], 2)
+    img = torch.randint(n_img, (n,), generator=g)
+    pix = torch.randint(H * W, (n,), generator=g)
+    ro, rd, imd = batch_rays(dirs.to(cuda), poses.to(cuda), img.to(cuda), pix.to(cuda))
+    P = poses.double()[img]
+    ref_d = (dirs.double()[pix][:, None, :] @ P[..., :3].transpose(1, 2))[:, 0]
+    ref_i = (dirs.double().mean(0)[None, None, :].expand(n, 1, 3) @ P[..., :3].transpose(1, 2))[:, 0]
+    assert torch.allclose(rd.cpu().double(), ref_d, atol=1e-6)
+    assert torch.equal(ro.cpu(), poses[img][..., 3])
+    assert torch.allclose(imd.cpu().double(), ref_i, atol=1e-6)
+    # single-pose form of get_rays
+    o1, d1 = get_rays(dirs.to(cuda), poses[0].to(cuda))
+    assert torch.allclose(d1.cpu().double(), dirs.double() @ poses[0, :, :3].double().T, atol=1e-6)
+    assert torch.equal(o1.cpu(), poses[0, :, 3].expand(H * W, 3))
