@@ -111,9 +111,15 @@ class _FieldFn(torch.autograd.Function):
         dev = xyzs.device
         sigma = torch.empty(n, device=dev)
         rgb = torch.empty(n, 3, device=dev)
+        # encoding cache for the backward (64 B/sample): only when a gradient
+        # will be asked for (density-grid updates run without)
+        feat = None
+        if n > 0 and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
+            feat = torch.empty((n + 31) // 32 * 32, 32, device=dev, dtype=torch.float16)
         if n > 0:
-            model._launch_field(True, xyzs, dirs, ind, sigma=sigma, rgb=rgb)
+            model._launch_field(True, xyzs, dirs, ind, sigma=sigma, rgb=rgb, feat=feat)
         ctx.save_for_backward(xyzs, dirs)
+        ctx.feat = feat
         ctx.model, ctx.ind = model, ind
         return sigma, rgb
 
@@ -128,7 +134,8 @@ class _FieldFn(torch.autograd.Function):
             ds = torch.zeros(xyzs.shape[0], device=dev) if dsigma is None else dsigma.float().contiguous()
             dr = torch.zeros(xyzs.shape[0], 3, device=dev) if drgb is None else drgb.float().contiguous()
             model._launch_field(False, xyzs, dirs, ind, dsigma=ds, drgb=dr, grid_grad=grid_grad,
-                                dw=dw)
+                                dw=dw, feat=ctx.feat)
+        ctx.feat = None
         return None, None, grid_grad, dw, None, None
 
 
@@ -190,7 +197,7 @@ class MNGP(nn.Module):
         return self._frags
 
     def _launch_field(self, fwd, xyzs, dirs, ind, sigma=None, rgb=None, dsigma=None, drgb=None,
-                      grid_grad=None, dw=None, blocks=None):
+                      grid_grad=None, dw=None, blocks=None, feat=None):
         dev = xyzs.device
         frags = self.packed_frags()
         grid16 = self.xyz_encoder.params_f16()
@@ -201,15 +208,15 @@ class MNGP(nn.Module):
             nb = blocks or max(1, min(2048, (n + 127) // 128))
             lib().field_fwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
                             None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
-                            self._h_ext.ctypes.data, fptr, sigma.data_ptr(), rgb.data_ptr(), None,
-                            nb, _stream(dev))
+                            self._h_ext.ctypes.data, fptr, sigma.data_ptr(), rgb.data_ptr(),
+                            None if feat is None else feat.data_ptr(), nb, _stream(dev))
         else:
             nb = blocks or max(1, min(256, (n + 255) // 256))
             lib().field_bwd(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None,
                             None, 1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
                             self._h_ext.ctypes.data, fptr, dsigma.data_ptr(), drgb.data_ptr(),
-                            grid_grad.data_ptr(), dw.data_ptr() + ind * LY.FIELD_PARAMS * 4, None,
-                            nb, _stream(dev))
+                            grid_grad.data_ptr(), dw.data_ptr() + ind * LY.FIELD_PARAMS * 4,
+                            None if feat is None else feat.data_ptr(), nb, _stream(dev))
 
     # ------------------------------------------------------------ reference API
     def density(self, x, ind, return_feat=False):
