@@ -33,6 +33,14 @@ int rn_ray_aabb_intersect(const float* rays_o, const float* rays_d, const float*
                           int32_t max_hits, int32_t* hit_cnt, float* hits_t,
                           int64_t* hits_voxel_idx, void* stream);
 
+/* ---- ray / sphere ------------------------------------------------------------
+ * replaces vren.ray_sphere_intersect (binding.cpp:19-31, intersection.cu:103-197):
+ * t_near clamped at 0, hits sorted by t_near like torch::sort (-1 slots first). */
+int rn_ray_sphere_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                            const float* radii, int64_t n_rays, int64_t n_spheres,
+                            int32_t max_hits, int32_t* hit_cnt, float* hits_t,
+                            int64_t* hits_sphere_idx, void* stream);
+
 /* ---- training ray march ----------------------------------------------------
  * replaces vren.raymarching_train (binding.cpp:60-81, raymarching.cu:166-332)
  * as three deterministic steps: count -> rn_scan_segments -> write.
@@ -48,6 +56,12 @@ int rn_raymarching_train_write(const float* rays_o, const float* rays_d, const f
                                int32_t max_samples, int64_t n_rays, const int32_t* counts,
                                const int32_t* offsets, int64_t* rays_a, float* xyzs, float* dirs,
                                float* deltas, float* ts, void* stream);
+
+/* RayMarcher.backward (custom_functions.py:102-112, torch_scatter.segment_csr):
+ * per rays_a row, dL_drays_o = sum dL_dxyzs, dL_drays_d = sum(dL_dxyzs*ts + dL_ddirs). */
+int rn_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, const float* ts,
+                            const int64_t* rays_a, int64_t n_rows, float* dL_drays_o,
+                            float* dL_drays_d, void* stream);
 
 /* exclusive scan of counts[n_seg][n_per]; segment k starts at an `align`
  * multiple: seg_base[k], seg_count[k]; meta[0] = aligned end, meta[1] = total.
@@ -107,6 +121,17 @@ int rn_composite_test_fw(const float* sigmas, const float* rgbs, const float* de
                          const float* ts, int64_t n_alive, int32_t n_samples,
                          int64_t* alive_indices, float T_threshold, const int32_t* n_eff_samples,
                          float* opacity, float* depth, float* rgb, void* stream);
+
+/* ---- distortion loss (Mip-NeRF 360 / DVGO-v2) ------------------------------
+ * replaces vren.distortion_loss_fw / _bw (binding.cpp:197-231, losses.cu:9-150).
+ * fw writes loss[rays_a[n][0]] and the per-sample inclusive scans of ws and
+ * ws*ts; bw consumes those scans (losses.py:6-36 DistortionLoss).            */
+int rn_distortion_loss_fw(const float* ws, const float* deltas, const float* ts,
+                          const int64_t* rays_a, int64_t n_rows, float* loss, float* ws_incl,
+                          float* wts_incl, void* stream);
+int rn_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const float* wts_incl,
+                          const float* ws, const float* deltas, const float* ts,
+                          const int64_t* rays_a, int64_t n_rows, float* dL_dws, void* stream);
 
 /* fused ml path: per-(model, ray) composite + gated combine
  * (ml_rendering.py:41-78 and the bg term of :192-200)                       */

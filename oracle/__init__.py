@@ -180,3 +180,45 @@ def ml_march(rays_o, rays_d, center, half_size, noise, bitfields, cascades, scal
     deltas = np.zeros(total, np.float32)
     L.oracle_ml_march(*args, I64(total), _p(counts), _p(starts), _p(xyzs), _p(ts), _p(deltas))
     return counts, starts, xyzs, ts, deltas, int(total)
+
+
+def ray_sphere_intersect(rays_o, rays_d, centers, radii, max_hits):
+    o, d, c, r = map(_f32, (rays_o, rays_d, centers, radii))
+    n = len(o)
+    cnt = np.zeros(n, np.int32)
+    ht = np.zeros((n, max_hits, 2), np.float32)
+    hi = np.zeros((n, max_hits), np.int64)
+    lib().oracle_ray_sphere_intersect(_p(o), _p(d), _p(c), _p(r), I64(n), I64(len(c)),
+                                      I32(max_hits), _p(cnt), _p(ht), _p(hi))
+    return cnt, ht, hi
+
+
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """losses.cu:62-110 -> loss (N_rays), ws_inclusive_scan, wts_inclusive_scan."""
+    w, dl, t = map(_f32, (ws, deltas, ts))
+    ra = np.ascontiguousarray(rays_a, dtype=np.int64)
+    loss = np.zeros(len(ra), np.float32)
+    wi = np.zeros(len(w), np.float32)
+    wti = np.zeros(len(w), np.float32)
+    lib().oracle_distortion_loss_fw(_p(w), _p(dl), _p(t), _p(ra), I64(len(ra)), _p(loss),
+                                    _p(wi), _p(wti))
+    return loss, wi, wti
+
+
+def distortion_loss_bw(dL_dloss, ws_incl, wts_incl, ws, deltas, ts, rays_a):
+    g, wi, wti, w, dl, t = map(_f32, (dL_dloss, ws_incl, wts_incl, ws, deltas, ts))
+    ra = np.ascontiguousarray(rays_a, dtype=np.int64)
+    out = np.zeros(len(w), np.float32)
+    lib().oracle_distortion_loss_bw(_p(g), _p(wi), _p(wti), _p(w), _p(dl), _p(t), _p(ra),
+                                    I64(len(ra)), _p(out))
+    return out
+
+
+def raymarching_train_bw(dL_dxyzs, dL_ddirs, ts, rays_a):
+    gx, gd, t = map(_f32, (dL_dxyzs, dL_ddirs, ts))
+    ra = np.ascontiguousarray(rays_a, dtype=np.int64)
+    go = np.zeros((len(ra), 3), np.float32)
+    gdir = np.zeros((len(ra), 3), np.float32)
+    lib().oracle_raymarching_train_bw(_p(gx), _p(gd), _p(t), _p(ra), I64(len(ra)), _p(go),
+                                      _p(gdir))
+    return go, gdir

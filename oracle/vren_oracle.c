@@ -380,3 +380,109 @@ int64_t oracle_ml_march(const float* rays_o, const float* rays_d, const float* c
     }
     return start;
 }
+
+/* intersection.cu:103-120 (_ray_sphere_intersect) + :123-150 (kernel) + :191-195
+ * (sort by t_near).  Deterministic sphere order, then a stable sort. */
+void oracle_ray_sphere_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                                 const float* radii, int64_t n_rays, int64_t n_sph, int max_hits,
+                                 int32_t* hit_cnt, float* hits_t, int64_t* hit_idx) {
+    for (int64_t r = 0; r < n_rays; ++r) {
+        const float* o = rays_o + 3 * r;
+        const float* d = rays_d + 3 * r;
+        float* ht = hits_t + r * max_hits * 2;
+        int64_t* hi = hit_idx + r * max_hits;
+        for (int m = 0; m < max_hits; ++m) { ht[2 * m] = -1.f; ht[2 * m + 1] = -1.f; hi[m] = -1; }
+        int cnt = 0;
+        for (int64_t s = 0; s < n_sph; ++s) {
+            const float cx = o[0] - centers[3 * s], cy = o[1] - centers[3 * s + 1],
+                        cz = o[2] - centers[3 * s + 2];
+            const float a = d[0] * d[0] + d[1] * d[1] + d[2] * d[2];
+            const float hb = d[0] * cx + d[1] * cy + d[2] * cz;
+            const float c = (cx * cx + cy * cy + cz * cz) - radii[s] * radii[s];
+            const float disc = hb * hb - a * c;
+            float t1 = -1.f, t2 = -1.f;
+            if (!(disc < 0)) {
+                const float q = sqrtf(disc);
+                t1 = (-hb - q) / a;
+                t2 = (-hb + q) / a;
+            }
+            if (t2 > 0) {
+                if (cnt < max_hits) { ht[2 * cnt] = fmaxf(t1, 0.0f); ht[2 * cnt + 1] = t2; hi[cnt] = s; }
+                cnt++;
+            }
+        }
+        hit_cnt[r] = cnt;
+        for (int a = 1; a < max_hits; ++a) {
+            float k0 = ht[2 * a], k1 = ht[2 * a + 1];
+            int64_t kv = hi[a];
+            int b = a - 1;
+            while (b >= 0 && ht[2 * b] > k0) {
+                ht[2 * (b + 1)] = ht[2 * b]; ht[2 * (b + 1) + 1] = ht[2 * b + 1]; hi[b + 1] = hi[b];
+                --b;
+            }
+            ht[2 * (b + 1)] = k0; ht[2 * (b + 1) + 1] = k1; hi[b + 1] = kv;
+        }
+    }
+}
+
+/* losses.cu:9-44 (prefix sums), :47-110 (distortion_loss_fw): per rays_a row,
+ * serial scans of ws and ws*ts, per-sample term
+ *   2*(wts_incl*ws_excl - ws_incl*wts_excl) + 1/3*ws*ws*deltas
+ * summed into loss[ray_idx].  loss (n_out) must be zeroed by the caller. */
+void oracle_distortion_loss_fw(const float* ws, const float* deltas, const float* ts,
+                               const int64_t* rays_a, int64_t n_rows, float* loss,
+                               float* ws_incl, float* wts_incl) {
+    for (int64_t n = 0; n < n_rows; ++n) {
+        const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+        float sw = 0.f, swt = 0.f, acc = 0.f;
+        for (int64_t i = 0; i < N; ++i) {
+            const int64_t s = start + i;
+            const float wt = ws[s] * ts[s];
+            const float ex_w = sw, ex_wt = swt;
+            sw += ws[s];
+            swt += wt;
+            ws_incl[s] = sw;
+            wts_incl[s] = swt;
+            const float term = 2.0f * (swt * ex_w - sw * ex_wt) +
+                               (1.0f / 3) * ws[s] * ws[s] * deltas[s];
+            acc += term;
+        }
+        loss[ray] = acc;
+    }
+}
+
+/* losses.cu:113-150 (distortion_loss_bw_kernel) */
+void oracle_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const float* wts_incl,
+                               const float* ws, const float* deltas, const float* ts,
+                               const int64_t* rays_a, int64_t n_rows, float* dL_dws) {
+    for (int64_t n = 0; n < n_rows; ++n) {
+        const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+        if (N <= 0) continue;
+        const int64_t end = start + N - 1;
+        const float ws_sum = ws_incl[end], wts_sum = wts_incl[end];
+        const float g = dL_dloss[ray];
+        for (int64_t s = start; s <= end; ++s) {
+            const float front = s == start ? 0.f : ts[s] * ws_incl[s - 1] - wts_incl[s - 1];
+            const float back = wts_sum - wts_incl[s] - ts[s] * (ws_sum - ws_incl[s]);
+            dL_dws[s] = g * 2 * (front + back);
+            dL_dws[s] += g * (2.0f / 3) * ws[s] * deltas[s];
+        }
+    }
+}
+
+/* custom_functions.py:102-112 (RayMarcher.backward, torch_scatter.segment_csr
+ * sums over the rays_a segments, in ray-row order) */
+void oracle_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, const float* ts,
+                                 const int64_t* rays_a, int64_t n_rows, float* dL_drays_o,
+                                 float* dL_drays_d) {
+    for (int64_t n = 0; n < n_rows; ++n) {
+        const int64_t start = rays_a[3 * n + 1], N = rays_a[3 * n + 2];
+        float o[3] = {0, 0, 0}, d[3] = {0, 0, 0};
+        for (int64_t s = start; s < start + N; ++s)
+            for (int c = 0; c < 3; ++c) {
+                o[c] += dL_dxyzs[3 * s + c];
+                d[c] += dL_dxyzs[3 * s + c] * ts[s] + dL_ddirs[3 * s + c];
+            }
+        for (int c = 0; c < 3; ++c) { dL_drays_o[3 * n + c] = o[c]; dL_drays_d[3 * n + c] = d[c]; }
+    }
+}

@@ -293,6 +293,73 @@ k_ml_composite_bw(int n_rays, int K, const float* __restrict__ gRGB,
                  gb, go, gd, dsig, drgb);
 }
 
+// ---------------------------------------------------------------------------
+// distortion loss (Mip-NeRF 360 / DVGO-v2), losses.cu:9-150.  The reference
+// runs four thrust scans per ray inside one thread plus torch elementwise ops
+// and a per-thread thrust::reduce; here one wave per rays_a row does the
+// scans as wave prefix sums and reduces the per-sample terms in registers.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_distortion_fw(int n_rows, const float* __restrict__ ws, const float* __restrict__ dl,
+                const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
+                float* __restrict__ loss, float* __restrict__ ws_incl,
+                float* __restrict__ wts_incl) {
+    const int row = blockIdx.x * (blockDim.x / RN_WAVE) + (threadIdx.x / RN_WAVE);
+    if (row >= n_rows) return;
+    const int lane = rn_lane();
+    const int64_t ray = rays_a[3 * row], start = rays_a[3 * row + 1];
+    const int n = (int)rays_a[3 * row + 2];
+    float pw = 0.f, pwt = 0.f, acc = 0.f;
+    for (int base = 0; base < n; base += RN_WAVE) {
+        const int i = base + lane;
+        const bool valid = i < n;
+        float w = 0.f, t = 0.f, d = 0.f;
+        if (valid) { w = ws[start + i]; t = ts[start + i]; d = dl[start + i]; }
+        const float wt = w * t;
+        const float sw = pw + rn_wave_incl_sum(w);
+        const float swt = pwt + rn_wave_incl_sum(wt);
+        float ex_w = __shfl_up(sw, 1), ex_wt = __shfl_up(swt, 1);   // exclusive scans
+        if (lane == 0) { ex_w = pw; ex_wt = pwt; }
+        if (valid) {
+            ws_incl[start + i] = sw;
+            wts_incl[start + i] = swt;
+            acc += 2.0f * (swt * ex_w - sw * ex_wt) + (1.0f / 3) * w * w * d;
+        }
+        pw = __shfl(sw, RN_WAVE - 1);
+        pwt = __shfl(swt, RN_WAVE - 1);
+    }
+    acc = rn_wave_sum(acc);
+    if (lane == 0) loss[ray] = acc;
+}
+
+__global__ void __launch_bounds__(256)
+k_distortion_bw(int n_rows, const float* __restrict__ dL_dloss,
+                const float* __restrict__ ws_incl, const float* __restrict__ wts_incl,
+                const float* __restrict__ ws, const float* __restrict__ dl,
+                const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
+                float* __restrict__ dL_dws) {
+    const int row = blockIdx.x * (blockDim.x / RN_WAVE) + (threadIdx.x / RN_WAVE);
+    if (row >= n_rows) return;
+    const int lane = rn_lane();
+    const int64_t ray = rays_a[3 * row], start = rays_a[3 * row + 1];
+    const int n = (int)rays_a[3 * row + 2];
+    if (n <= 0) return;
+    const int64_t end = start + n - 1;
+    const float ws_sum = ws_incl[end], wts_sum = wts_incl[end];
+    const float g = dL_dloss[ray];
+    for (int base = 0; base < n; base += RN_WAVE) {
+        const int i = base + lane;
+        if (i >= n) break;
+        const int64_t s = start + i;
+        const float t = ts[s];
+        const float front = i == 0 ? 0.f : t * ws_incl[s - 1] - wts_incl[s - 1];
+        const float back = wts_sum - wts_incl[s] - t * (ws_sum - ws_incl[s]);
+        float v = g * 2 * (front + back);
+        v += g * (2.0f / 3) * ws[s] * dl[s];
+        dL_dws[s] = v;
+    }
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -398,6 +465,31 @@ int rn_ml_composite_bw(const float* dL_drgb, const float* dL_dopacity, const flo
     k_ml_composite_bw<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, dL_drgb, dL_dopacity, dL_ddepth, gate, bg, sigmas, rgbs, deltas,
         ts, counts, offsets, opacity_k, depth_k, rgb_k, T_threshold, dL_dsigmas, dL_drgbs);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_distortion_loss_fw(const float* ws, const float* deltas, const float* ts,
+                          const int64_t* rays_a, int64_t n_rows, float* loss, float* ws_incl,
+                          float* wts_incl, void* stream) {
+    RN_CHECK_ARG(n_rows >= 0, "bad sizes");
+    if (n_rows == 0) return 0;
+    RN_CHECK_ARG(ws && deltas && ts && rays_a && loss && ws_incl && wts_incl, "null pointer");
+    k_distortion_fw<<<nblk(n_rows, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rows, ws, deltas, ts, rays_a, loss, ws_incl, wts_incl);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_distortion_loss_bw(const float* dL_dloss, const float* ws_incl, const float* wts_incl,
+                          const float* ws, const float* deltas, const float* ts,
+                          const int64_t* rays_a, int64_t n_rows, float* dL_dws, void* stream) {
+    RN_CHECK_ARG(n_rows >= 0, "bad sizes");
+    if (n_rows == 0) return 0;
+    RN_CHECK_ARG(dL_dloss && ws_incl && wts_incl && ws && deltas && ts && rays_a && dL_dws,
+                 "null pointer");
+    k_distortion_bw<<<nblk(n_rows, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rows, dL_dloss, ws_incl, wts_incl, ws, deltas, ts, rays_a, dL_dws);
     RN_CHECK_LAUNCH();
     return 0;
 }

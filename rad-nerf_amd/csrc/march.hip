@@ -468,6 +468,81 @@ inline MarchCfg make_cfg(int cascades, int grid_size, int max_samples, float sca
     return c;
 }
 
+// intersection.cu:103-150 (ray/sphere) with the t_near sort of :191-195.
+__global__ void __launch_bounds__(256)
+k_ray_sphere(int n_rays, int n_sph, int max_hits, const float* __restrict__ rays_o,
+             const float* __restrict__ rays_d, const float* __restrict__ centers,
+             const float* __restrict__ radii, int32_t* __restrict__ hit_cnt,
+             float* __restrict__ hits_t, int64_t* __restrict__ hit_idx) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= n_rays) return;
+    const float ox = rays_o[3 * r], oy = rays_o[3 * r + 1], oz = rays_o[3 * r + 2];
+    const float dx = rays_d[3 * r], dy = rays_d[3 * r + 1], dz = rays_d[3 * r + 2];
+    float* ht = hits_t + (size_t)r * max_hits * 2;
+    int64_t* hi = hit_idx + (size_t)r * max_hits;
+    for (int m = 0; m < max_hits; ++m) { ht[2 * m] = -1.0f; ht[2 * m + 1] = -1.0f; hi[m] = -1; }
+    const float a = dx * dx + dy * dy + dz * dz;
+    int cnt = 0;
+    for (int v = 0; v < n_sph; ++v) {
+        const float cx = ox - centers[3 * v], cy = oy - centers[3 * v + 1],
+                    cz = oz - centers[3 * v + 2];
+        const float hb = dx * cx + dy * cy + dz * cz;
+        const float c = (cx * cx + cy * cy + cz * cz) - radii[v] * radii[v];
+        const float disc = hb * hb - a * c;
+        float t1 = -1.0f, t2 = -1.0f;
+        if (!(disc < 0)) {
+            const float q = sqrtf(disc);
+            t1 = (-hb - q) / a;
+            t2 = (-hb + q) / a;
+        }
+        if (t2 > 0) {
+            if (cnt < max_hits) {
+                ht[2 * cnt] = fmaxf(t1, 0.0f); ht[2 * cnt + 1] = t2; hi[cnt] = v;
+            }
+            cnt++;
+        }
+    }
+    hit_cnt[r] = cnt;
+    for (int i = 1; i < max_hits; ++i) {
+        const float k0 = ht[2 * i], k1 = ht[2 * i + 1];
+        const int64_t kv = hi[i];
+        int b = i - 1;
+        while (b >= 0 && ht[2 * b] > k0) {
+            ht[2 * (b + 1)] = ht[2 * b]; ht[2 * (b + 1) + 1] = ht[2 * b + 1]; hi[b + 1] = hi[b];
+            --b;
+        }
+        ht[2 * (b + 1)] = k0; ht[2 * (b + 1) + 1] = k1; hi[b + 1] = kv;
+    }
+}
+
+// RayMarcher.backward (custom_functions.py:102-112, torch_scatter.segment_csr):
+// per rays_a row, dL/drays_o = sum dL/dxyz and dL/drays_d = sum (dL/dxyz * t +
+// dL/ddir) over the row's samples.  One wave per row, coalesced strided reads.
+__global__ void __launch_bounds__(256)
+k_march_train_bw(int n_rows, const float* __restrict__ gx, const float* __restrict__ gd,
+                 const float* __restrict__ ts, const int64_t* __restrict__ rays_a,
+                 float* __restrict__ go, float* __restrict__ gdir) {
+    const int row = blockIdx.x * (blockDim.x / RN_WAVE) + (threadIdx.x / RN_WAVE);
+    if (row >= n_rows) return;
+    const int lane = rn_lane();
+    const int64_t start = rays_a[3 * row + 1];
+    const int n = (int)rays_a[3 * row + 2];
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    for (int i = lane; i < n; i += RN_WAVE) {
+        const int64_t s = start + i;
+        const float t = ts[s];
+        const float x0 = gx[3 * s], x1 = gx[3 * s + 1], x2 = gx[3 * s + 2];
+        o0 += x0; o1 += x1; o2 += x2;
+        d0 += x0 * t + gd[3 * s]; d1 += x1 * t + gd[3 * s + 1]; d2 += x2 * t + gd[3 * s + 2];
+    }
+    o0 = rn_wave_sum(o0); o1 = rn_wave_sum(o1); o2 = rn_wave_sum(o2);
+    d0 = rn_wave_sum(d0); d1 = rn_wave_sum(d1); d2 = rn_wave_sum(d2);
+    if (lane == 0) {
+        go[3 * row] = o0; go[3 * row + 1] = o1; go[3 * row + 2] = o2;
+        gdir[3 * row] = d0; gdir[3 * row + 1] = d1; gdir[3 * row + 2] = d2;
+    }
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -616,6 +691,34 @@ int rn_ml_compact(const int32_t* counts, const int32_t* offsets, int64_t n_rays,
     k_ml_compact<<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, max_samples, counts, offsets, stage_ts, stage_deltas, ts, deltas,
         ray_of);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_ray_sphere_intersect(const float* rays_o, const float* rays_d, const float* centers,
+                            const float* radii, int64_t n_rays, int64_t n_spheres,
+                            int32_t max_hits, int32_t* hit_cnt, float* hits_t,
+                            int64_t* hits_sphere_idx, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_spheres >= 0 && max_hits >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(rays_o && rays_d && hit_cnt && hits_t && hits_sphere_idx, "null pointer");
+    RN_CHECK_ARG(n_spheres == 0 || (centers && radii), "null pointer");
+    k_ray_sphere<<<nblk(n_rays, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, (int)n_spheres, max_hits, rays_o, rays_d, centers, radii, hit_cnt, hits_t,
+        hits_sphere_idx);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, const float* ts,
+                            const int64_t* rays_a, int64_t n_rows, float* dL_drays_o,
+                            float* dL_drays_d, void* stream) {
+    RN_CHECK_ARG(n_rows >= 0, "bad sizes");
+    if (n_rows == 0) return 0;
+    RN_CHECK_ARG(dL_dxyzs && dL_ddirs && ts && rays_a && dL_drays_o && dL_drays_d,
+                 "null pointer");
+    k_march_train_bw<<<nblk(n_rows, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rows, dL_dxyzs, dL_ddirs, ts, rays_a, dL_drays_o, dL_drays_d);
     RN_CHECK_LAUNCH();
     return 0;
 }

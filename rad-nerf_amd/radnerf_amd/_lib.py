@@ -20,6 +20,10 @@ F32 = ctypes.c_float
 # name -> argtypes (all return int status).  Keep in sync with include/radnerf.h
 SIGNATURES = {
     "rn_ray_aabb_intersect": [P, P, P, P, I64, I64, I32, P, P, P, P],
+    "rn_ray_sphere_intersect": [P, P, P, P, I64, I64, I32, P, P, P, P],
+    "rn_raymarching_train_bw": [P, P, P, P, I64, P, P, P],
+    "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
+    "rn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
     "rn_raymarching_train_count": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P],
     "rn_raymarching_train_write": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P, P, P, P,
                                    P, P, P],

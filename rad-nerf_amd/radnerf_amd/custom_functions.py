@@ -44,11 +44,9 @@ class RayMarcher(torch.autograd.Function):
         # in the reference, custom_functions.py:107-110); only live with
         # --optimize_ext.  rays_a here is in ray order, so segments are sorted.
         rays_a, ts = ctx.saved_tensors
-        lengths = rays_a[:, 2]
-        dL_drays_o = torch.segment_reduce(dL_dxyzs, "sum", lengths=lengths, axis=0,
-                                          unsafe=True)
-        dL_drays_d = torch.segment_reduce(dL_dxyzs * ts[:, None] + dL_ddirs, "sum",
-                                          lengths=lengths, axis=0, unsafe=True)
+        z = lambda g: torch.zeros(ts.shape[0], 3, device=ts.device) if g is None \
+            else g.float().contiguous()
+        dL_drays_o, dL_drays_d = vren.raymarching_train_bw(z(dL_dxyzs), z(dL_ddirs), ts, rays_a)
         return dL_drays_o, dL_drays_d, None, None, None, None, None, None, None, None
 
 

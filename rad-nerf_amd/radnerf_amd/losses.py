@@ -8,30 +8,59 @@
                    `sum(term.mean())`; FusedMLRenderer.train_step feeds them
                    straight into the fused backward (no autograd graph).
 
-The distortion (vren.distortion_loss_*) and disparity terms default to 0 in
-train_ml.py and are out of scope.
+`DistortionLoss`    the reference autograd Function (losses.py:6-36) on the HIP
+                   distortion kernels (vren.distortion_loss_fw / _bw).
 """
 import torch
 from torch import nn
 
+from . import vren
 from ._lib import lib
 
 
+class DistortionLoss(torch.autograd.Function):
+    """losses.py:6-36: Mip-NeRF 360 distortion loss (DVGO-v2 form) per ray.
+    Inputs ws, deltas, ts (N) and rays_a (N_rays, 3); output loss (N_rays)."""
+
+    @staticmethod
+    def forward(ctx, ws, deltas, ts, rays_a):
+        loss, ws_incl, wts_incl = vren.distortion_loss_fw(
+            ws.float().contiguous(), deltas.float().contiguous(), ts.float().contiguous(),
+            rays_a.contiguous())
+        ctx.save_for_backward(ws_incl, wts_incl, ws, deltas, ts, rays_a)
+        return loss
+
+    @staticmethod
+    def backward(ctx, dL_dloss):
+        ws_incl, wts_incl, ws, deltas, ts, rays_a = ctx.saved_tensors
+        dL_dws = vren.distortion_loss_bw(dL_dloss.float().contiguous(), ws_incl, wts_incl,
+                                         ws.float().contiguous(), deltas.float().contiguous(),
+                                         ts.float().contiguous(), rays_a.contiguous())
+        return dL_dws, None, None, None
+
+
 class NeRFLoss(nn.Module):
-    """losses.py:39-76 (without the distortion / disparity terms)."""
+    """losses.py:39-76."""
 
     def __init__(self, lambda_opacity=1e-3):
         super().__init__()
 
     def forward(self, results, target, lambda_opacity=1e-3, lambda_distortion=0, lambda_disp=0,
                 lambda_cv_importance=0, lambda_depth_mutual=0):
-        if lambda_distortion > 0 or lambda_disp > 0:
-            raise NotImplementedError("distortion / disparity losses are out of scope")
         loss = {}
         loss["rgb"] = (results["rgb"] - target["rgb"]) ** 2
         o = results["opacity"] + 1e-10
         loss["opacity"] = lambda_opacity * (-o * torch.log(o))
+        if lambda_disp > 0:
+            loss["disp"] = lambda_disp * results["disp"] ** 2
         K = results["gating_code"].shape[-1]
+        if lambda_distortion > 0:
+            # per sub-NeRF keys ws_i / deltas_i / ts_i / rays_a_i (losses.py:63-67)
+            loss["distortion"] = 0
+            for i in range(K):
+                loss["distortion"] += lambda_distortion * DistortionLoss.apply(
+                    results[f"ws_{i}"], results[f"deltas_{i}"], results[f"ts_{i}"],
+                    results[f"rays_a_{i}"]).mean()
         if lambda_cv_importance > 0 and K > 1:
             imp = results["gating_importance"].float()
             loss["cv_importance"] = lambda_cv_importance * imp.var() / (imp.mean() ** 2 + 1e-10)

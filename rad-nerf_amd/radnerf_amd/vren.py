@@ -186,15 +186,63 @@ def packbits(density_grid, density_threshold, density_bitfield):
                    _p(density_bitfield), _stream(density_grid))
 
 
-def distortion_loss_fw(*args, **kwargs):
-    raise NotImplementedError("distortion_loss_fw: out of scope for this build (SURVEY.md §2: "
-                              "dead in Rad-NeRF, distortion_loss_w defaults to 0)")
+def distortion_loss_fw(ws, deltas, ts, rays_a):
+    """binding.cpp:197-209, losses.cu:62-110 -> [loss (N_rays), ws_inclusive_scan (N),
+    wts_inclusive_scan (N)]; loss is indexed by rays_a[:, 0]."""
+    for n, t in (("ws", ws), ("deltas", deltas), ("ts", ts)):
+        _check_f32(n, t)
+    _check("rays_a", rays_a)
+    n_rows, N = rays_a.shape[0], ws.shape[0]
+    dev = ws.device
+    loss = torch.zeros(n_rows, device=dev)
+    ws_incl = torch.zeros(N, device=dev)
+    wts_incl = torch.zeros(N, device=dev)
+    lib().distortion_loss_fw(_p(ws), _p(deltas), _p(ts), _p(rays_a), n_rows, _p(loss),
+                             _p(ws_incl), _p(wts_incl), _stream(ws))
+    return [loss, ws_incl, wts_incl]
 
 
-def distortion_loss_bw(*args, **kwargs):
-    raise NotImplementedError("distortion_loss_bw: out of scope for this build")
+def distortion_loss_bw(dL_dloss, ws_inclusive_scan, wts_inclusive_scan, ws, deltas, ts, rays_a):
+    """binding.cpp:212-231, losses.cu:113-150 -> dL_dws (N)"""
+    for n, t in (("dL_dloss", dL_dloss), ("ws_inclusive_scan", ws_inclusive_scan),
+                 ("wts_inclusive_scan", wts_inclusive_scan), ("ws", ws), ("deltas", deltas),
+                 ("ts", ts)):
+        _check_f32(n, t)
+    _check("rays_a", rays_a)
+    dL_dws = torch.zeros(ws.shape[0], device=ws.device)
+    lib().distortion_loss_bw(_p(dL_dloss), _p(ws_inclusive_scan), _p(wts_inclusive_scan),
+                             _p(ws), _p(deltas), _p(ts), _p(rays_a), rays_a.shape[0],
+                             _p(dL_dws), _stream(ws))
+    return dL_dws
 
 
-def ray_sphere_intersect(*args, **kwargs):
-    raise NotImplementedError("ray_sphere_intersect: never called on the Rad-NeRF path "
-                              "(SURVEY.md §2)")
+def ray_sphere_intersect(rays_o, rays_d, centers, radii, max_hits):
+    """binding.cpp:19-31, intersection.cu:153-197 -> [hit_cnt i32 (N), hits_t f32
+    (N,max_hits,2), hits_sphere_idx i64 (N,max_hits)]"""
+    for n, t in (("rays_o", rays_o), ("rays_d", rays_d), ("centers", centers),
+                 ("radii", radii)):
+        _check_f32(n, t)
+    n_rays, n_sph = rays_o.shape[0], centers.shape[0]
+    dev = rays_o.device
+    hit_cnt = torch.empty(n_rays, dtype=torch.int32, device=dev)
+    hits_t = torch.empty(n_rays, max_hits, 2, dtype=torch.float32, device=dev)
+    hits_idx = torch.empty(n_rays, max_hits, dtype=torch.int64, device=dev)
+    lib().ray_sphere_intersect(_p(rays_o), _p(rays_d), _p(centers), _p(radii), n_rays, n_sph,
+                               int(max_hits), _p(hit_cnt), _p(hits_t), _p(hits_idx),
+                               _stream(rays_o))
+    return [hit_cnt, hits_t, hits_idx]
+
+
+def raymarching_train_bw(dL_dxyzs, dL_ddirs, ts, rays_a):
+    """RayMarcher.backward's segment_csr pair (custom_functions.py:107-110) in one
+    launch -> [dL_drays_o (N_rows,3), dL_drays_d (N_rows,3)].  Not a reference vren
+    export: the reference calls torch_scatter here."""
+    for n, t in (("dL_dxyzs", dL_dxyzs), ("dL_ddirs", dL_ddirs), ("ts", ts)):
+        _check_f32(n, t)
+    _check("rays_a", rays_a)
+    n_rows = rays_a.shape[0]
+    go = torch.empty(n_rows, 3, device=ts.device)
+    gd = torch.empty(n_rows, 3, device=ts.device)
+    lib().raymarching_train_bw(_p(dL_dxyzs), _p(dL_ddirs), _p(ts), _p(rays_a), n_rows, _p(go),
+                               _p(gd), _stream(ts))
+    return [go, gd]

@@ -67,8 +67,12 @@ def test_vren_checks_like_reference():
     with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
         vren.composite_train_fw(torch.zeros(4), cpu, torch.zeros(4), torch.zeros(4),
                                 torch.zeros(1, 3, dtype=torch.long), 1e-4)
-    with pytest.raises(NotImplementedError):
-        vren.distortion_loss_fw()
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        vren.distortion_loss_fw(torch.zeros(4), torch.zeros(4), torch.zeros(4),
+                                torch.zeros(1, 3, dtype=torch.long))
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        vren.ray_sphere_intersect(torch.zeros(1, 3), torch.zeros(1, 3), torch.zeros(1, 3),
+                                  torch.ones(1), 1)
 
 
 def test_missing_library_fails_loudly(tmp_path, monkeypatch):
