@@ -182,6 +182,40 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  const float* dL_drgb, float* grid_grad, float* dw, const void* feat_cache,
                  int32_t blocks_per_model, void* stream);
 
+/* ---- merged field backward (fused training path) ------------------------
+ * Same gradients as rn_field_bwd over the compact layout of rn_ml_compact,
+ * but the hash-grid gradient of the K sub-NeRFs (which share the grid) is
+ * scattered in merged per-ray (ray, t) order, so samples of different models
+ * on one ray share atomic requests.
+ * rn_bwd_plan builds the merged order (mstart [n_rays + 1] i32, perm [total]
+ * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: chunks of
+ * max_chunk merged samples for the first 7/8 of the work, then min_chunk;
+ * queue [2] i32 = ticket, chunk count).  cap_chunks must bound the chunk
+ * count: >= total/max_chunk + total/(8*min_chunk) + 2.
+ * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
+ * stages 144-B rows in its scratch slice (scratch: blocks x scratch_rows x 36
+ * f32, scratch_rows >= max_chunk + n_models * max_samples) and parks per-model
+ * dW accumulators in park (blocks x n_models x 16384 f32).
+ * Replaces, with rn_field_bwd, the backward of the tcnn modules called at
+ * models/networks.py:300-328 (autograd sums the K sub-NeRFs' gradients into
+ * the shared xyz_encoder's).                                               */
+int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
+                const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
+                int32_t max_chunk, int32_t min_chunk, int32_t cap_chunks, int32_t* mstart,
+                int32_t* perm, int32_t* chunk_first, int32_t* queue, void* stream);
+int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
+                        const int32_t* chunk_first, int32_t* queue, int64_t n_rays,
+                        int32_t n_models, int32_t max_samples,
+                        const void* grid_f16, const uint32_t* level_offset,
+                        const uint32_t* level_hsize, const uint32_t* level_res,
+                        const float* level_scale, const float* xyz_min, const float* extent,
+                        const void* frags, const float* dL_dsigma, const float* dL_drgb,
+                        float* grid_grad, float* dw, const void* feat_cache, float* scratch,
+                        int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
+                        void* stream);
+
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------
  * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)
  * as (x, x+3, 6) or rays_o/rays_d as (rays_o, rays_d, 3).  importance (K) is

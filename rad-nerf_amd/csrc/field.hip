@@ -315,24 +315,19 @@ __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __exp
 
 enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2 };
 
+// forward of one 32-sample tile for the lanes' samples `s` (valid lanes only
+// load); fc: this lane's encoding-cache slot (CACHE_WRITE writes it on every
+// lane, CACHE_READ reads it on valid lanes)
 template <int MODE, int CACHE>
-__device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T, const rn_half* W,
-                                             int64_t base, int64_t n, int64_t tile, FwdState& st,
-                                             bool& valid, int64_t& s, float& ux, float& uy,
-                                             float& uz) {
-    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
-    const int64_t i = tile * 32 + c;
-    valid = i < n;
-    s = base + (valid ? i : 0);
+__device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& T, const rn_half* W,
+                                               int64_t s, bool valid, half8* fc, FwdState& st,
+                                               float& ux, float& uy, float& uz) {
+    const int h = rn_lane() >> 5;
     float x = 0.f, y = 0.f, z = 0.f, dx = 1.f, dy = 0.f, dz = 0.f;
     if (valid) load_sample<MODE>(a, s, x, y, z, dx, dy, dz);
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-    // the encoding cache is indexed by 32-sample tile of the global sample
-    // array (segment bases are 128-aligned); lane-linear, 32 B per lane
-    half8* fc = CACHE == CACHE_NONE ? nullptr
-              : reinterpret_cast<half8*>(a.feat) + (((base >> 5) + tile) * 64 + lane) * 2;
     if (CACHE == CACHE_READ) {
         // lanes past the segment end (the backward walks whole 8-tile
         // iterations) were never written: zero encoding, as the gather path
@@ -345,6 +340,28 @@ __device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T,
     }
     st.sh = sh_lane(dx, dy, dz, h);
     mlp_forward(W, st);
+}
+
+// encoding-cache slot of global sample s: 32-sample tiles of the sample
+// array, lane-linear (lane c + 32h holds sample c's k-steps of half h)
+__device__ __forceinline__ half8* cache_slot(const FieldArgs& a, int64_t s) {
+    return reinterpret_cast<half8*>(a.feat) + ((s >> 5) * 64 + (s & 31) + 32 * (rn_lane() >> 5)) * 2;
+}
+
+template <int MODE, int CACHE>
+__device__ __forceinline__ void tile_forward(const FieldArgs& a, const LvTab& T, const rn_half* W,
+                                             int64_t base, int64_t n, int64_t tile, FwdState& st,
+                                             bool& valid, int64_t& s, float& ux, float& uy,
+                                             float& uz) {
+    const int lane = rn_lane(), c = lane & 31;
+    const int64_t i = tile * 32 + c;
+    valid = i < n;
+    s = base + (valid ? i : 0);
+    // the encoding cache is indexed by 32-sample tile of the global sample
+    // array (segment bases are 128-aligned); lane-linear, 32 B per lane
+    half8* fc = CACHE == CACHE_NONE ? nullptr
+              : reinterpret_cast<half8*>(a.feat) + (((base >> 5) + tile) * 64 + lane) * 2;
+    tile_forward_s<MODE, CACHE>(a, T, W, s, valid, fc, st, ux, uy, uz);
 }
 
 template <int MODE, int CACHE>
@@ -480,17 +497,22 @@ __device__ __forceinline__ void ring_drain(ScatterRing& R, uint32_t min_cnt,
     }
 }
 
-// Walk of one wave over the block's 256 samples.  Lane = (stream, corner):
-// stream = (quarter of the samples, level w or 15-w), one lane per corner
-// holding both features.  Each lane walks its 64 samples in ray order.
+// Walk of one wave over the block's 256 samples.  Lane = (stream, parity
+// class): stream = (quarter of the samples, level w or 15-w), and each of the
+// stream's 8 lanes tracks the current cell's corner of one parity class
+// p = (X & 1, Y & 1, Z & 1) (every cell has exactly one corner per class), so
+// when the cell moves, the lane's corner either stays the same entry (it is
+// shared by the two cells: keep accumulating) or leaves (emit it) -- a lane-
+// local test, no data moves between lanes.  Each lane walks its 64 samples in
+// ray order holding both features of its entry.
 __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvTab& sT,
                                                    const float* sG, const float* sU, int nblk,
                                                    ScatterRing& R,
                                                    __amdgpu_buffer_rsrc_t grad_rs) {
     const int lane = rn_lane();
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-    const int stream = lane >> 3, quarter = stream >> 1, corner = lane & 7;
-    const int cx = corner & 1, cy = (corner >> 1) & 1, cz = corner >> 2;
+    const int stream = lane >> 3, quarter = stream >> 1, par = lane & 7;
+    const uint32_t px = par & 1, py = (par >> 1) & 1, pz = par >> 2;
     const int l = (stream & 1) ? (RN_L - 1 - wid) : wid;
     const LvConst lc = lv_const(sT, a.gm, l);
     const uint64_t smask = 0xffull << (8 * stream);
@@ -499,7 +521,7 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
     const int nq = max(0, min(QN, nblk - quarter * QN));
     const int s_base = quarter * QN;
     const float* gcol = sG + 2 * l;
-    int gx = -1000, gy = 0, gz = 0;                       // current cell (none yet)
+    uint32_t ex = 0xffffffffu, ey = 0, ez = 0;            // current entry coords (none yet)
     uint32_t cur = 0;
     float acc0 = 0.f, acc1 = 0.f;
     // software pipeline: this step's sample row is loaded one step ahead
@@ -516,27 +538,24 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
             un = *reinterpret_cast<const float4*>(sU + nx * 4);
             gn = *reinterpret_cast<const float2*>(gcol + nx * SG_STRIDE);
             const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
-            const float w = corner_weight(p, corner);
-            const int dx = (int)p.gx - gx, dy = (int)p.gy - gy, dz = (int)p.gz - gz;
-            // new corner c <- old corner c + delta (if that is a corner of the old cell)
-            const int ox = cx + dx, oy = cy + dy, oz = cz + dz;
-            const bool src_ok = (unsigned)ox <= 1u && (unsigned)oy <= 1u && (unsigned)oz <= 1u;
-            const int src = (lane & ~7) | (src_ok ? ox + 2 * oy + 4 * oz : 0);
-            const float c0 = __shfl(acc0, src), c1 = __shfl(acc1, src);
-            // old corner c survives as new corner c - delta
-            const int mx = cx - dx, my = cy - dy, mz = cz - dz;
-            const bool keep = (unsigned)mx <= 1u && (unsigned)my <= 1u && (unsigned)mz <= 1u;
-            ring_push(R, act && !keep && gx != -1000, smask, 8u * (lc.off + cur), acc0, acc1);
+            // this class's corner of the cell: the one of {g, g+1} with parity p
+            const uint32_t cx = (px ^ p.gx) & 1u, cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
+            const uint32_t X = p.gx + cx, Y = p.gy + cy, Z = p.gz + cz;
+            const float w = (cx ? p.fx : 1.0f - p.fx) * (cy ? p.fy : 1.0f - p.fy) *
+                            (cz ? p.fz : 1.0f - p.fz);
+            const bool same = X == ex && Y == ey && Z == ez;
+            ring_push(R, act && !same && ex != 0xffffffffu, smask, 8u * (lc.off + cur), acc0,
+                      acc1);
             if (act) {
-                acc0 = (src_ok ? c0 : 0.f) + w * gc.x;
-                acc1 = (src_ok ? c1 : 0.f) + w * gc.y;
-                cur = corner_index(lc, p, corner);
-                gx = (int)p.gx; gy = (int)p.gy; gz = (int)p.gz;
+                acc0 = (same ? acc0 : 0.f) + w * gc.x;
+                acc1 = (same ? acc1 : 0.f) + w * gc.y;
+                cur = grid_index(lc, X, Y, Z);
+                ex = X; ey = Y; ez = Z;
             }
         }
         ring_drain(R, 32u, grad_rs, a.dbg);
     }
-    ring_push(R, gx != -1000, smask, 8u * (lc.off + cur), acc0, acc1);
+    ring_push(R, ex != 0xffffffffu, smask, 8u * (lc.off + cur), acc0, acc1);
     ring_drain(R, 32u, grad_rs, a.dbg);
 }
 
@@ -568,6 +587,159 @@ __device__ __forceinline__ void dw_flush(const f32x16& acc, float* dw, int off, 
     }
 }
 
+// flush a wave's owned dW tiles (ownership table in k_field_bwd) into dw
+__device__ __forceinline__ void dw_flush_owned(const f32x16& accA, const f32x16& accB, float* dw,
+                                               int wid, float inv) {
+    if (wid < 2) {
+        dw_flush<DW_ROWS_LT3>(accA, dw, 9280, 64, 0, 32 * wid, inv);   // rgb3
+        dw_flush<DW_GEO>(accB, dw, 2048, 64, 0, 32 * wid, inv);        // geo2
+    } else if (wid < 6) {
+        const int mm = (wid - 2) >> 1, nn = (wid - 2) & 1;
+        dw_flush<DW_PLAIN>(accA, dw, 5184, 64, 32 * mm, 32 * nn, inv); // rgb2
+        if (wid < 4) dw_flush<DW_PLAIN>(accB, dw, 0, 32, 32 * (wid - 2), 0, inv);  // geo1
+    } else {
+        dw_flush<DW_PLAIN>(accA, dw, 3136, 32, 32 * (wid - 6), 0, inv); // rgb1
+    }
+}
+
+// Backward of one block iteration (8 waves x 32-sample tiles, the tiles'
+// forward state in `st`): seeds -> block gradient scale -> dX chain on MFMA
+// with the block-cooperative dW tiles (accA/accB at cur_scale, rescaled
+// exactly when the scale changes).  Returns dL/dencoding at scale `gscale`
+// (rows in MFMA accumulator order); zero_iter: all 256 seeds are zero.
+__device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* sW,
+                                             const rn_half* sImg, float* sMax, rn_half* imgY,
+                                             rn_half* imgX, FwdState& st, bool valid, int64_t s,
+                                             int wid, f32x16& accA, f32x16& accB,
+                                             float& cur_scale, bool do_dw, float& gscale_out,
+                                             bool& zero_iter_out) {
+    const int lane = rn_lane(), h = lane >> 5;
+    const half8 z8 = rn_zero8();
+    // ---- seeds (lanes h == 0 own the output rows)
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
+    if (valid && h == 0) {
+        const float ds = a.dsigma[s];
+        const float y0 = sigmoidf(st.out[0]), y1 = sigmoidf(st.out[1]),
+                    y2 = sigmoidf(st.out[2]);
+        o0 = a.drgb[3 * s] * (y0 * (1.0f - y0));        // sigmoid'
+        o1 = a.drgb[3 * s + 1] * (y1 * (1.0f - y1));
+        o2 = a.drgb[3 * s + 2] * (y2 * (1.0f - y2));
+        // TruncExp.backward: g * exp(clamp(x, -15, 15))  (custom_functions.py:171-173)
+        gsig = ds * expf(fminf(fmaxf(st.g0, -15.f), 15.f));
+    }
+    float m = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(gsig)));
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    if (lane == 0) sMax[wid] = m;
+    __syncthreads();                                                    // B0
+    float bm = sMax[0];
+#pragma unroll
+    for (int w = 1; w < BWD_WAVES; ++w) bm = fmaxf(bm, sMax[w]);
+    // an iteration whose 256 samples all have zero seeds (samples past the
+    // early-termination point of their rays, volumerendering.cu:150) adds
+    // nothing to the hash grid: its scatter walk is skipped (an early
+    // `continue` of the whole iteration made the compiler spill 190 B/lane)
+    const bool zero_iter = bm == 0.f;
+    const float gscale = rn_wave_grad_scale(bm);   // uniform over the block
+    if (cur_scale != gscale) {                     // exact power-of-two rescale
+        const float r = cur_scale == 0.f ? 0.f : gscale / cur_scale;
+        accA *= r; accB *= r;
+        cur_scale = gscale;
+    }
+    half8 dO = z8;
+    if (h == 0) {
+        dO[0] = (rn_half)(o0 * gscale);
+        dO[1] = (rn_half)(o1 * gscale);
+        dO[2] = (rn_half)(o2 * gscale);
+    }
+    // ---- layer rgb3: dW (w0, w1) = dO x R2 ; dR2 = Wr3^T dO masked
+    if (do_dw) {
+        rn_img_write(imgY, 0, dO); rn_img_write(imgY, 1, z8);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.r2[q]);
+    }
+    __syncthreads();                                                    // B1
+    if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
+    half8 dr2f[4];
+    {
+        f32x16 b0 = rn_zero16(), b1 = rn_zero16();
+        b0 = rn_mfma(rn_frag(sW, 24), dO, b0);
+        b1 = rn_mfma(rn_frag(sW, 25), dO, b1);
+        rn_acc_to_frags_masked(b0, st.r2[0], st.r2[1], dr2f[0], dr2f[1]);
+        rn_acc_to_frags_masked(b1, st.r2[2], st.r2[3], dr2f[2], dr2f[3]);
+    }
+    __syncthreads();                                                    // B2
+    // ---- layer rgb2: dW (w2..w5) = dR2 x R1 ; dR1 = Wr2^T dR2 masked
+    if (do_dw) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) { rn_img_write(imgY, q, dr2f[q]); rn_img_write(imgX, q, st.r1[q]); }
+    }
+    __syncthreads();                                                    // B3
+    if (do_dw && wid >= 2 && wid < 6)
+        accA = dw_block_tile(sImg, 32 * ((wid - 2) >> 1), 32 * ((wid - 2) & 1), accA);
+    half8 dr1f[4];
+    {
+        f32x16 b0 = rn_zero16(), b1 = rn_zero16();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            b0 = rn_mfma(rn_frag(sW, 26 + q), dr2f[q], b0);
+            b1 = rn_mfma(rn_frag(sW, 30 + q), dr2f[q], b1);
+        }
+        rn_acc_to_frags_masked(b0, st.r1[0], st.r1[1], dr1f[0], dr1f[1]);
+        rn_acc_to_frags_masked(b1, st.r1[2], st.r1[3], dr1f[2], dr1f[3]);
+    }
+    __syncthreads();                                                    // B4
+    // ---- layer rgb1: dW (w6, w7) = dR1 x [SH | geo 1..16] ; dG
+    if (do_dw) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dr1f[q]);
+        rn_img_write(imgX, 0, st.sh); rn_img_write(imgX, 1, st.gin);
+    }
+    __syncthreads();                                                    // B5
+    if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
+    half8 dg0, dg1;
+    {
+        f32x16 b = rn_zero16();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b = rn_mfma(rn_frag(sW, 34 + q), dr1f[q], b);
+        if (h == 0) b[8] = gsig * gscale;          // row 16 = dL/dh0
+        rn_acc_to_frags<false>(b, dg0, dg1);
+    }
+    __syncthreads();                                                    // B6
+    // ---- layer geo2: dW (w0, w1) = dG x H1 ; dH1 = Wg2^T dG masked
+    if (do_dw) {
+        rn_img_write(imgY, 0, dg0); rn_img_write(imgY, 1, dg1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h1[q]);
+    }
+    __syncthreads();                                                    // B7
+    if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
+    half8 dh1f[4];
+    {
+        f32x16 b0 = rn_zero16(), b1 = rn_zero16();
+        b0 = rn_mfma(rn_frag(sW, 38), dg0, b0); b0 = rn_mfma(rn_frag(sW, 39), dg1, b0);
+        b1 = rn_mfma(rn_frag(sW, 40), dg0, b1); b1 = rn_mfma(rn_frag(sW, 41), dg1, b1);
+        rn_acc_to_frags_masked(b0, st.h1[0], st.h1[1], dh1f[0], dh1f[1]);
+        rn_acc_to_frags_masked(b1, st.h1[2], st.h1[3], dh1f[2], dh1f[3]);
+    }
+    __syncthreads();                                                    // B8
+    // ---- layer geo1: dW (w2, w3) = dH1 x E ; dE = Wg1^T dH1
+    if (do_dw) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dh1f[q]);
+        rn_img_write(imgX, 0, st.e0); rn_img_write(imgX, 1, st.e1);
+    }
+    __syncthreads();                                                    // B9
+    if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
+    f32x16 dE = rn_zero16();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
+    __syncthreads();                                                    // B10
+    gscale_out = gscale;
+    zero_iter_out = zero_iter;
+    return dE;
+}
+
 template <int MODE, int CACHE>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
 k_field_bwd(FieldArgs a) {
@@ -590,7 +762,6 @@ k_field_bwd(FieldArgs a) {
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
     rn_half* imgX = imgY + RN_IMG_HALFS;
-    const half8 z8 = rn_zero8();
     const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
     const bool do_dw = !(a.dbg & 2);
 
@@ -620,126 +791,9 @@ k_field_bwd(FieldArgs a) {
         bool valid; int64_t s; float ux, uy, uz;
         tile_forward<MODE, CACHE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
 
-        // ---- seeds (lanes h == 0 own the output rows)
-        float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
-        if (valid && h == 0) {
-            const float ds = a.dsigma[s];
-            const float y0 = sigmoidf(st.out[0]), y1 = sigmoidf(st.out[1]),
-                        y2 = sigmoidf(st.out[2]);
-            o0 = a.drgb[3 * s] * (y0 * (1.0f - y0));        // sigmoid'
-            o1 = a.drgb[3 * s + 1] * (y1 * (1.0f - y1));
-            o2 = a.drgb[3 * s + 2] * (y2 * (1.0f - y2));
-            // TruncExp.backward: g * exp(clamp(x, -15, 15))  (custom_functions.py:171-173)
-            gsig = ds * expf(fminf(fmaxf(st.g0, -15.f), 15.f));
-        }
-        float m = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(gsig)));
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-        if (lane == 0) sMax[wid] = m;
-        __syncthreads();                                                    // B0
-        float bm = sMax[0];
-#pragma unroll
-        for (int w = 1; w < BWD_WAVES; ++w) bm = fmaxf(bm, sMax[w]);
-        // an iteration whose 256 samples all have zero seeds (samples past the
-        // early-termination point of their rays, volumerendering.cu:150) adds
-        // nothing to the hash grid: its scatter walk is skipped (an early
-        // `continue` of the whole iteration made the compiler spill 190 B/lane)
-        const bool zero_iter = bm == 0.f;
-        const float gscale = rn_wave_grad_scale(bm);   // uniform over the block
-        if (cur_scale != gscale) {                     // exact power-of-two rescale
-            const float r = cur_scale == 0.f ? 0.f : gscale / cur_scale;
-            accA *= r; accB *= r;
-            cur_scale = gscale;
-        }
-        half8 dO = z8;
-        if (h == 0) {
-            dO[0] = (rn_half)(o0 * gscale);
-            dO[1] = (rn_half)(o1 * gscale);
-            dO[2] = (rn_half)(o2 * gscale);
-        }
-        // ---- layer rgb3: dW (w0, w1) = dO x R2 ; dR2 = Wr3^T dO masked
-        if (do_dw) {
-            rn_img_write(imgY, 0, dO); rn_img_write(imgY, 1, z8);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.r2[q]);
-        }
-        __syncthreads();                                                    // B1
-        if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
-        half8 dr2f[4];
-        {
-            f32x16 b0 = rn_zero16(), b1 = rn_zero16();
-            b0 = rn_mfma(rn_frag(sW, 24), dO, b0);
-            b1 = rn_mfma(rn_frag(sW, 25), dO, b1);
-            rn_acc_to_frags_masked(b0, st.r2[0], st.r2[1], dr2f[0], dr2f[1]);
-            rn_acc_to_frags_masked(b1, st.r2[2], st.r2[3], dr2f[2], dr2f[3]);
-        }
-        __syncthreads();                                                    // B2
-        // ---- layer rgb2: dW (w2..w5) = dR2 x R1 ; dR1 = Wr2^T dR2 masked
-        if (do_dw) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) { rn_img_write(imgY, q, dr2f[q]); rn_img_write(imgX, q, st.r1[q]); }
-        }
-        __syncthreads();                                                    // B3
-        if (do_dw && wid >= 2 && wid < 6)
-            accA = dw_block_tile(sImg, 32 * ((wid - 2) >> 1), 32 * ((wid - 2) & 1), accA);
-        half8 dr1f[4];
-        {
-            f32x16 b0 = rn_zero16(), b1 = rn_zero16();
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                b0 = rn_mfma(rn_frag(sW, 26 + q), dr2f[q], b0);
-                b1 = rn_mfma(rn_frag(sW, 30 + q), dr2f[q], b1);
-            }
-            rn_acc_to_frags_masked(b0, st.r1[0], st.r1[1], dr1f[0], dr1f[1]);
-            rn_acc_to_frags_masked(b1, st.r1[2], st.r1[3], dr1f[2], dr1f[3]);
-        }
-        __syncthreads();                                                    // B4
-        // ---- layer rgb1: dW (w6, w7) = dR1 x [SH | geo 1..16] ; dG
-        if (do_dw) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dr1f[q]);
-            rn_img_write(imgX, 0, st.sh); rn_img_write(imgX, 1, st.gin);
-        }
-        __syncthreads();                                                    // B5
-        if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
-        half8 dg0, dg1;
-        {
-            f32x16 b = rn_zero16();
-#pragma unroll
-            for (int q = 0; q < 4; ++q) b = rn_mfma(rn_frag(sW, 34 + q), dr1f[q], b);
-            if (h == 0) b[8] = gsig * gscale;          // row 16 = dL/dh0
-            rn_acc_to_frags<false>(b, dg0, dg1);
-        }
-        __syncthreads();                                                    // B6
-        // ---- layer geo2: dW (w0, w1) = dG x H1 ; dH1 = Wg2^T dG masked
-        if (do_dw) {
-            rn_img_write(imgY, 0, dg0); rn_img_write(imgY, 1, dg1);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h1[q]);
-        }
-        __syncthreads();                                                    // B7
-        if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
-        half8 dh1f[4];
-        {
-            f32x16 b0 = rn_zero16(), b1 = rn_zero16();
-            b0 = rn_mfma(rn_frag(sW, 38), dg0, b0); b0 = rn_mfma(rn_frag(sW, 39), dg1, b0);
-            b1 = rn_mfma(rn_frag(sW, 40), dg0, b1); b1 = rn_mfma(rn_frag(sW, 41), dg1, b1);
-            rn_acc_to_frags_masked(b0, st.h1[0], st.h1[1], dh1f[0], dh1f[1]);
-            rn_acc_to_frags_masked(b1, st.h1[2], st.h1[3], dh1f[2], dh1f[3]);
-        }
-        __syncthreads();                                                    // B8
-        // ---- layer geo1: dW (w2, w3) = dH1 x E ; dE = Wg1^T dH1
-        if (do_dw) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dh1f[q]);
-            rn_img_write(imgX, 0, st.e0); rn_img_write(imgX, 1, st.e1);
-        }
-        __syncthreads();                                                    // B9
-        if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
-        f32x16 dE = rn_zero16();
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
-        __syncthreads();                                                    // B10
+        float gscale; bool zero_iter;
+        const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid, accA, accB,
+                                     cur_scale, do_dw, gscale, zero_iter);
 
         // ---- hash-grid gradient scatter (grid_scatter_block)
         if (do_sc && !zero_iter) {
@@ -759,20 +813,294 @@ k_field_bwd(FieldArgs a) {
     }
     if (do_sc) ring_drain(R, 0u, grad_rs, a.dbg);
     // ---- flush the owned dW tiles
-    if (cur_scale != 0.f && do_dw) {
-        float* dw = a.dw + (size_t)k * FIELD_PARAMS;
-        const float inv = 1.0f / cur_scale;
-        if (wid < 2) {
-            dw_flush<DW_ROWS_LT3>(accA, dw, 9280, 64, 0, 32 * wid, inv);   // rgb3
-            dw_flush<DW_GEO>(accB, dw, 2048, 64, 0, 32 * wid, inv);        // geo2
-        } else if (wid < 6) {
-            const int mm = (wid - 2) >> 1, nn = (wid - 2) & 1;
-            dw_flush<DW_PLAIN>(accA, dw, 5184, 64, 32 * mm, 32 * nn, inv); // rgb2
-            if (wid < 4) dw_flush<DW_PLAIN>(accB, dw, 0, 32, 32 * (wid - 2), 0, inv);  // geo1
-        } else {
-            dw_flush<DW_PLAIN>(accA, dw, 3136, 32, 32 * (wid - 6), 0, inv); // rgb1
+    if (cur_scale != 0.f && do_dw) dw_flush_owned(accA, accB, a.dw + (size_t)k * FIELD_PARAMS, wid,
+                                                   1.0f / cur_scale);
+}
+
+// ---------------------------------------------------------------------------
+// Merged backward: the K sub-NeRFs share the hash grid, and the samples of the
+// K models on one ray visit the same cells.  k_field_bwd scatters each model's
+// samples separately (one stream per (model, ray)); here a block owns a CHUNK
+// of rays for all K models and scatters their samples merged in (ray, t)
+// order, so consecutive samples of different models share 64-B segments and
+// the atomic requests per sample drop (tools/atomic_sim.py on the bench
+// workload: per-(model, ray) floor 19.3 -> 12.9 per ray for K = 2).
+//
+// Per chunk [r0, r1) (grabbed from a guided work queue over rays):
+//  1. for each model k (alternating order, so one switch per chunk boundary):
+//     switch the block to model k (park the other model's dW accumulators in
+//     a per-block global area, reload the weights), then run the MLP backward
+//     over model k's samples of the chunk in 8-tile windows (bwd_window) and
+//     stage dL/dencoding + unit coords as 144-B rows in the block's scratch;
+//  2. walk the chunk's merged order (perm, from rn_bwd_plan) in windows of 256
+//     samples: rows -> LDS (sG/sU) -> grid_scatter_block, unchanged.
+// The grid gradient is the same sum as k_field_bwd's (float atomics: equal up
+// to summation order); dW is identical per model.
+// ---------------------------------------------------------------------------
+#define MB_ROW 36          // scratch row floats: dE[32] | ux uy uz | pad
+#define MB_KMAX 8
+
+struct MergeArgs {
+    const int32_t* offsets;  // [K][B] first sample of (model, ray)
+    const int32_t* mstart;   // [B + 1] first merged position of ray r; [B] = total
+    const int32_t* perm;     // [total] merged position -> sample index
+    const int32_t* chunk_first;  // [n_chunks + 1] first ray of each chunk; [n] = B
+    int32_t* queue;          // [0] ticket counter, [1] n_chunks (rn_bwd_plan)
+    float* scratch;          // [gridDim.x][rows_cap][MB_ROW]
+    float* park;             // [gridDim.x][K][BWD_WAVES][32][64]
+    int32_t n_rays, n_models, rows_cap;
+};
+
+// wave's dW accumulators <-> its park slot (lane-linear, 32 x 256 B)
+__device__ __forceinline__ void dw_park(float* p, const f32x16& A, const f32x16& B) {
+    const int lane = rn_lane();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { p[j * 64 + lane] = A[j]; p[(16 + j) * 64 + lane] = B[j]; }
+}
+__device__ __forceinline__ void dw_unpark(const float* p, f32x16& A, f32x16& B) {
+    const int lane = rn_lane();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        A[j] = __builtin_nontemporal_load(p + j * 64 + lane);
+        B[j] = __builtin_nontemporal_load(p + (16 + j) * 64 + lane);
+    }
+}
+
+template <int CACHE>
+__global__ void __launch_bounds__(BWD_WAVES * 64)
+k_field_bwd_merged(FieldArgs a, MergeArgs m) {
+    __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
+    __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
+    __shared__ float sMax[BWD_WAVES];
+    __shared__ LvTab sT;
+    __shared__ uint32_t sRing[BWD_WAVES * SC_STREAMS * 3 * SC_RING];
+    __shared__ float sScale[MB_KMAX];           // per model: scale of its parked dW (0 = none)
+    // chunk descriptor: r0, r1, then per model: first sample, count, row offset, segment base
+    __shared__ int32_t sCh[2 + 4 * MB_KMAX];
+    const int K = m.n_models, B = m.n_rays;
+    lv_stage(sT, a.gm);
+    if (threadIdx.x < MB_KMAX) sScale[threadIdx.x] = 0.f;
+
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
+    rn_half* imgX = imgY + RN_IMG_HALFS;
+    const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
+    const bool do_dw = !(a.dbg & 2);
+    const bool do_sc = !(a.dbg & 4);
+    float* sG = reinterpret_cast<float*>(sImg);
+    float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;
+    ScatterRing R;
+    R.ring = sRing + wid * SC_STREAMS * 3 * SC_RING;
+#pragma unroll
+    for (int q = 0; q < SC_STREAMS; ++q) R.head[q] = 0;
+    R.tail = 0;
+
+    f32x16 accA = rn_zero16(), accB = rn_zero16();
+    float cur_scale = 0.f;
+    int cur_k = -1;
+    float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
+    float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
+    int n_local = 0;
+
+    for (;;) {
+        __syncthreads();                         // previous chunk done with sCh / LDS
+        if (threadIdx.x == 0) {
+            // next non-empty chunk of the plan (rn_bwd_plan's chunk list)
+            const int n_chunks = m.queue[1];
+            int r0 = B, r1 = B;
+            for (;;) {
+                const int ch = atomicAdd(m.queue, 1);
+                if (ch >= n_chunks) break;
+                r0 = m.chunk_first[ch]; r1 = m.chunk_first[ch + 1];
+                if (r1 > r0) break;
+                r0 = B;
+            }
+            sCh[0] = r0; sCh[1] = r1;
+            int roff = 0;
+            for (int k = 0; k < K; ++k) {
+                const int sb = a.seg_base[k];
+                const int a0 = r0 < B ? m.offsets[k * B + r0] : 0;
+                const int a1 = r1 < B ? m.offsets[k * B + r1] : sb + a.seg_count[k];
+                sCh[2 + k] = a0; sCh[2 + MB_KMAX + k] = r0 < B ? a1 - a0 : 0;
+                sCh[2 + 2 * MB_KMAX + k] = roff; sCh[2 + 3 * MB_KMAX + k] = sb;
+                roff += r0 < B ? a1 - a0 : 0;
+            }
+        }
+        __syncthreads();
+        const int r0 = sCh[0], r1 = sCh[1];
+        if (r0 >= B) break;
+        const bool rev = n_local & 1;
+        ++n_local;
+
+        // ---- 1. MLP backward per model, rows staged in the block's scratch
+        for (int kk = 0; kk < K; ++kk) {
+            const int k = rev ? K - 1 - kk : kk;
+            const int a_k = sCh[2 + k], n_k = sCh[2 + MB_KMAX + k], roff = sCh[2 + 2 * MB_KMAX + k];
+            if (n_k == 0) continue;
+            if (k != cur_k) {
+                __syncthreads();                 // every wave done with sW
+                if (cur_k >= 0) {
+                    dw_park(park + (size_t)cur_k * BWD_WAVES * 2048, accA, accB);
+                    if (threadIdx.x == 0) sScale[cur_k] = cur_scale;
+                }
+                rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
+                                FIELD_FRAGS * RN_FRAG_BYTES);
+                __syncthreads();
+                cur_scale = sScale[k];
+                if (cur_scale != 0.f) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, accA, accB);
+                else { accA = rn_zero16(); accB = rn_zero16(); }
+                cur_k = k;
+            }
+            for (int w0 = 0; w0 < n_k; w0 += BWD_WAVES * 32) {
+                rn_lds_order();
+                const int i = w0 + wid * 32 + c;
+                const bool valid = i < n_k;
+                const int64_t s = a_k + (valid ? i : 0);
+                FwdState st;
+                float ux, uy, uz;
+                tile_forward_s<1, CACHE>(a, sT, sW, s, valid,
+                                         CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, st,
+                                         ux, uy, uz);
+                float gscale; bool zero_iter;
+                const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid,
+                                             accA, accB, cur_scale, do_dw, gscale, zero_iter);
+                if (valid) {
+                    const float ginv = zero_iter ? 0.f : 1.0f / gscale;
+                    float* row = rows + (size_t)(roff + i) * MB_ROW;
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {   // features 8g + 4h .. +3 = dE[4g .. 4g+3]
+                        *reinterpret_cast<float4*>(row + 8 * g + 4 * h) =
+                            make_float4(dE[4 * g] * ginv, dE[4 * g + 1] * ginv,
+                                        dE[4 * g + 2] * ginv, dE[4 * g + 3] * ginv);
+                    }
+                    if (h == 0) *reinterpret_cast<float4*>(row + 32) = make_float4(ux, uy, uz, 0.f);
+                }
+            }
+        }
+        if (!do_sc) continue;
+
+        // ---- 2. scatter in merged (ray, t) order
+        __builtin_amdgcn_s_waitcnt(0x0070);     // vmcnt(0): this wave's rows are in L2
+        __syncthreads();
+        const int p_base = m.mstart[r0], n_p = m.mstart[r1] - p_base;
+        for (int p0 = 0; p0 < n_p; p0 += BWD_WAVES * 32) {
+            const int nblk = min(BWD_WAVES * 32, n_p - p0);
+            const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
+            int nz = 0;
+            if (j < nblk) {
+                const int smp = m.perm[p_base + p0 + j];
+                int k = 0;
+                for (int q = 1; q < K; ++q) k = smp >= sCh[2 + 3 * MB_KMAX + q] ? q : k;
+                const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
+                // rows were written by other waves of this block: read past L1 (nt)
+                typedef float nf4 __attribute__((ext_vector_type(4)));
+                const nf4* src = reinterpret_cast<const nf4*>(rows + (size_t)row_i * MB_ROW)
+                                 + 4 * half;
+                float* dst = sG + j * SG_STRIDE + 16 * half;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const nf4 v = __builtin_nontemporal_load(src + q);
+                    *reinterpret_cast<float2*>(dst + 4 * q) = make_float2(v.x, v.y);
+                    *reinterpret_cast<float2*>(dst + 4 * q + 2) = make_float2(v.z, v.w);
+                    nz |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
+                }
+                if (half) {
+                    const nf4 u = __builtin_nontemporal_load(
+                        reinterpret_cast<const nf4*>(rows + (size_t)row_i * MB_ROW) + 8);
+                    *reinterpret_cast<nf4*>(sU + j * 4) = u;
+                }
+            }
+            // a window whose rows are all zero (rays past early termination)
+            // adds nothing to the grid
+            if (__syncthreads_or(nz)) grid_scatter_block(a, sT, sG, sU, nblk, R, grad_rs);
+            __syncthreads();
         }
     }
+    if (do_sc) ring_drain(R, 0u, grad_rs, a.dbg);
+    // ---- flush every model's dW (the current one from registers)
+    if (do_dw) {
+        for (int k = 0; k < K; ++k) {
+            float sc = sScale[k];
+            f32x16 A, Bm;
+            if (k == cur_k) { sc = cur_scale; A = accA; Bm = accB; }
+            else if (sc != 0.f) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, A, Bm);
+            if (sc != 0.f) dw_flush_owned(A, Bm, a.dw + (size_t)k * FIELD_PARAMS, wid, 1.0f / sc);
+        }
+    }
+}
+
+// Merged order of the K models' samples per ray (ray-major, then t, ties by
+// model): perm[mstart[r] + rank] = sample.  One wave per ray; each sample's
+// rank = its index in its (model, ray) run + the samples of the other models
+// of the ray that precede it (binary search; t increases along a run).
+__global__ void __launch_bounds__(256)
+k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
+           const int32_t* __restrict__ seg_base, const int32_t* __restrict__ seg_count,
+           const float* __restrict__ ts, int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
+    const int r = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;
+    if (r >= B) return;
+    const int lane = rn_lane();
+    int ms = 0;
+    for (int k = 0; k < K; ++k) ms += offsets[k * B + r] - seg_base[k];
+    if (lane == 0) {
+        mstart[r] = ms;
+        if (r == 0) {
+            int tot = 0;
+            for (int k = 0; k < K; ++k) tot += seg_count[k];
+            mstart[B] = tot;
+        }
+    }
+    for (int k = 0; k < K; ++k) {
+        const int n = counts[k * B + r], o = offsets[k * B + r];
+        for (int i = lane; i < n; i += RN_WAVE) {
+            const float t = ts[o + i];
+            int pos = i;
+            for (int k2 = 0; k2 < K; ++k2) {
+                if (k2 == k) continue;
+                const int n2 = counts[k2 * B + r], o2 = offsets[k2 * B + r];
+                int lo = 0, hi = n2;             // count of t2 < t (k2 > k) or t2 <= t (k2 < k)
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    const float t2 = ts[o2 + mid];
+                    if (t2 < t || (k2 < k && t2 == t)) lo = mid + 1; else hi = mid;
+                }
+                pos += lo;
+            }
+            perm[ms + pos] = o + i;
+        }
+    }
+}
+
+// Chunk schedule of the merged backward over the merged positions [0, total):
+// chunks of max_chunk positions for the first 7/8 of the work, then chunks of
+// min_chunk (a short tail: blocks finish together).  Chunk c holds the rays
+// whose merged start lies in [bound(c), bound(c+1)), so it is whole rays of
+// at most max_chunk + K * max_samples samples (possibly none).
+__device__ __forceinline__ void chunk_plan(int total, int max_chunk, int min_chunk, int& c1,
+                                           int& n_chunks) {
+    c1 = (total - total / 8) / max_chunk;
+    const int rest = total - c1 * max_chunk;
+    n_chunks = c1 + (rest + min_chunk - 1) / min_chunk;
+}
+
+__global__ void __launch_bounds__(256)
+k_bwd_chunks(int B, const int32_t* __restrict__ mstart, int max_chunk, int min_chunk,
+             int cap_chunks, int32_t* __restrict__ chunk_first, int32_t* __restrict__ queue) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    const int total = mstart[B];
+    int c1, n;
+    chunk_plan(total, max_chunk, min_chunk, c1, n);
+    if (c == 0) { queue[0] = 0; queue[1] = n < cap_chunks ? n : cap_chunks; }
+    if (c > n || c > cap_chunks) return;
+    if (c == n || c == cap_chunks) { chunk_first[c] = B; return; }
+    const int bound = c <= c1 ? c * max_chunk : c1 * max_chunk + (c - c1) * min_chunk;
+    int lo = 0, hi = B;                       // first ray with mstart >= bound
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (mstart[mid] < bound) lo = mid + 1; else hi = mid;
+    }
+    chunk_first[c] = lo;
 }
 
 // dst[k][i] = idx[i] >= 0 ? f16(src[k][idx[i]]) : 0
@@ -905,6 +1233,64 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
         if (feat_cache) k_field_bwd<1, CACHE_READ><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
         else k_field_bwd<1, CACHE_NONE><<<grid, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     }
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
+                const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
+                int32_t max_chunk, int32_t min_chunk, int32_t cap_chunks, int32_t* mstart,
+                int32_t* perm, int32_t* chunk_first, int32_t* queue, void* stream) {
+    RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX, "bad sizes");
+    RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1, "bad chunk sizes");
+    RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
+                 chunk_first && queue, "null pointer");
+    k_bwd_plan<<<nblk(n_rays, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
+    RN_CHECK_LAUNCH();
+    k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, mstart, max_chunk, min_chunk, cap_chunks, chunk_first, queue);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
+                        const int32_t* chunk_first, int32_t* queue, int64_t n_rays,
+                        int32_t n_models, int32_t max_samples,
+                        const void* grid_f16, const uint32_t* level_offset,
+                        const uint32_t* level_hsize, const uint32_t* level_res,
+                        const float* level_scale, const float* xyz_min, const float* extent,
+                        const void* frags, const float* dL_dsigma, const float* dL_drgb,
+                        float* grid_grad, float* dw, const void* feat_cache, float* scratch,
+                        int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
+                        void* stream) {
+    RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX && blocks >= 1 &&
+                 max_samples >= 1 && max_chunk >= 1, "bad sizes");
+    RN_CHECK_ARG(scratch_rows >= (int64_t)max_chunk + (int64_t)n_models * max_samples,
+                 "scratch_rows must be >= max_chunk + n_models * max_samples");
+    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets && mstart &&
+                 perm && chunk_first && queue && grid_f16 && level_offset && level_hsize && level_res &&
+                 level_scale && xyz_min && extent && frags && dL_dsigma && dL_drgb && grid_grad &&
+                 dw && scratch && park, "null pointer");
+    FieldArgs a{};
+    fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
+    a.dbg = g_field_dbg;
+    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
+    a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
+    a.feat = (rn_half*)feat_cache;
+    a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
+    a.seg_base = seg_base; a.seg_count = seg_count;
+    MergeArgs m{};
+    m.offsets = offsets; m.mstart = mstart; m.perm = perm; m.chunk_first = chunk_first;
+    m.queue = queue;
+    m.scratch = scratch; m.park = park;
+    m.n_rays = (int)n_rays; m.n_models = n_models; m.rows_cap = (int)scratch_rows;
+    if (feat_cache)
+        k_field_bwd_merged<CACHE_READ><<<blocks, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a, m);
+    else
+        k_field_bwd_merged<CACHE_NONE><<<blocks, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a, m);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -58,6 +58,29 @@ class Workspace:
         self.stage_dt = torch.empty(K * B * max_samples, **f)
         # field fwd -> bwd encoding cache: 32 f16 per sample slot (64 B)
         self.feat = torch.empty((cap + 31) // 32 * 32, 32, device=device, dtype=torch.float16)
+        # merged backward (rn_bwd_plan): per-ray merged starts, merged order, queue head
+        self.mstart = torch.empty(B + 1, **i)
+        self.perm = torch.empty(cap, **i)
+        self.queue = torch.zeros(2, **i)
+        self._bwd_scratch = None
+        self._chunks = None
+
+    def chunk_list(self, max_chunk, min_chunk):
+        """rn_bwd_plan's chunk list, sized for the workspace capacity."""
+        cap = self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2
+        if self._chunks is None or self._chunks.numel() < cap + 1:
+            self._chunks = torch.empty(cap + 1, device=self.device, dtype=torch.int32)
+        return cap, self._chunks
+
+    def bwd_scratch(self, blocks, max_chunk, max_samples=MAX_SAMPLES):
+        """Per-block row scratch and dW park area of rn_field_bwd_merged."""
+        rows = max_chunk + self.K * max_samples
+        key = (blocks, rows)
+        if self._bwd_scratch is None or self._bwd_scratch[0] != key:
+            f = dict(device=self.device, dtype=torch.float32)
+            self._bwd_scratch = (key, torch.empty(blocks * rows * 36, **f),
+                                 torch.empty(blocks * self.K * 8 * 2048, **f))
+        return rows, self._bwd_scratch[1], self._bwd_scratch[2]
 
     @property
     def seg_base(self):
@@ -90,6 +113,12 @@ class FusedMLRenderer:
         self.fwd_blocks = fwd_blocks or max(1, 2048 // K)
         self.bwd_blocks = bwd_blocks or max(1, 256 // K)
         self.feat_cache = True      # field fwd stores the encoding, bwd skips the re-gather
+        # backward scatters the K models' grid gradients merged per ray
+        # (rn_field_bwd_merged); False: one model per block (rn_field_bwd)
+        self.merged_bwd = True
+        self.merged_blocks = 256
+        self.max_chunk = 4096
+        self.min_chunk = 512
         self.trace = False          # record HIP events around every launch
         self.events = {}
 
@@ -181,6 +210,23 @@ class FusedMLRenderer:
         if fwd:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
                      w.feat.data_ptr() if self.feat_cache else None, self.fwd_blocks, st)
+        elif self.merged_bwd:
+            rows, scratch, park = w.bwd_scratch(self.merged_blocks, self.max_chunk)
+            min_chunk = min(self.min_chunk, self.max_chunk)
+            cap, chunks = w.chunk_list(self.max_chunk, min_chunk)
+            self._ev("bwd_plan", L.bwd_plan, w.counts.data_ptr(), w.offsets.data_ptr(),
+                     w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, m.size,
+                     self.max_chunk, min_chunk, cap, w.mstart.data_ptr(), w.perm.data_ptr(),
+                     chunks.data_ptr(), w.queue.data_ptr(), st)
+            self._ev("field_bwd", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
+                     rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
+                     w.seg_count.data_ptr(), w.offsets.data_ptr(), w.mstart.data_ptr(),
+                     w.perm.data_ptr(), chunks.data_ptr(), w.queue.data_ptr(), w.B, m.size,
+                     MAX_SAMPLES,
+                     *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
+                     dw.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
+                     scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
+                     self.merged_blocks, st)
         else:
             self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
                      w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),

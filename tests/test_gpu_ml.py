@@ -127,3 +127,63 @@ def test_fused_full_size_properties(cuda):
     # determinism of the forward (no atomics on the forward path)
     res2 = ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
     assert torch.equal(res["rgb"], res2["rgb"])
+
+
+def _merged_vs_split(cuda, B, K, scale, p=0.5):
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale, p=p)
+    r = get_renderer(m, g, B)
+    out = []
+    for merged in (True, False):
+        r.merged_bwd = merged
+        _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+        out.append(gr)
+    r.merged_bwd = True
+    return r, out
+
+
+@pytest.mark.parametrize("B,K,scale", [(8192, 2, 0.5), (2048, 4, 16.0), (1024, 1, 0.5),
+                                       (512, 8, 0.5)])
+def test_merged_backward_matches_per_model(cuda, B, K, scale):
+    """rn_field_bwd_merged (K models' grid gradients scattered merged per ray)
+    vs rn_field_bwd (one model per block): the same sums in another order."""
+    r, (gm, gs) = _merged_vs_split(cuda, B, K, scale)
+    for a, b in zip(gm, gs):
+        rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+        assert rel <= 1e-5, rel
+    # merged order: ray-major, then t, ties by model (bit-exact)
+    w = r.ws
+    cnt = w.counts.cpu().numpy().astype(np.int64)
+    off = w.offsets.cpu().numpy().astype(np.int64)
+    ts = w.ts.cpu().numpy()
+    smp, ray, mod = [], [], []
+    for k in range(K):
+        for rr in range(B):
+            n = cnt[k, rr]
+            smp.append(np.arange(off[k, rr], off[k, rr] + n)); ray.append(np.full(n, rr))
+            mod.append(np.full(n, k))
+    smp, ray, mod = map(np.concatenate, (smp, ray, mod))
+    order = np.lexsort((mod, ts[smp], ray))
+    total = len(smp)
+    assert int(w.mstart[B]) == total
+    assert np.array_equal(w.perm[:total].cpu().numpy(), smp[order])
+    ms = w.mstart[:B].cpu().numpy()
+    assert np.array_equal(ms, np.concatenate([[0], np.cumsum(cnt.sum(0))[:-1]]))
+
+
+def test_merged_backward_chunking(cuda):
+    """Small chunks (many queue grabs, single-ray chunks above max_chunk) give
+    the same gradients."""
+    B, K = 2048, 2
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
+    r = get_renderer(m, g, B)
+    res = []
+    for mc, blocks in ((4096, 256), (64, 37), (300, 3)):
+        r.max_chunk, r.merged_blocks = mc, blocks
+        _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
+        res.append(gr)
+    r.max_chunk, r.merged_blocks = 4096, 256
+    for other in res[1:]:
+        for a, b in zip(other, res[0]):
+            rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+            assert rel <= 1e-5, rel

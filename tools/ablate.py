@@ -39,12 +39,14 @@ def main():
     r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
     L = lib()
     st = torch.cuda.current_stream().cuda_stream
-    # tokens: "<flags>" = field_bwd with debug flags, "f<flags>" = field_fwd
+    # tokens: "<flags>" = field_bwd (merged) with debug flags, "s<flags>" = the
+    # per-model field_bwd, "f<flags>" = field_fwd
     times = {f: [] for f in flags}
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(int(f.lstrip("f")))
+            L.set_debug_flags(int(f.lstrip("fs")))
+            r.merged_bwd = not f.startswith("s")
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             if f.startswith("f"):

@@ -1,0 +1,127 @@
+// Microbenchmark: rate of global scatter-add forms on gfx950 for the
+// hash-grid gradient access shape (wave instructions covering a few random
+// 64-B segments of a 45.7 MB table, like k_field_bwd's ring issue).
+// Question asked: do any forms (int32 adds, workgroup scope, XCD-private
+// copies of the table) execute in L2 instead of at the memory side, i.e. run
+// above the ~20 G requests/s float-atomic ceiling?
+//
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/atomic_probe tools/atomic_probe.hip
+// run:   tools/atomic_probe            (prints one line per variant)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+    printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); return 1; } } while (0)
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return v & 0xf;
+}
+
+// VAR: 0 f32 atomic agent, 1 f32 atomic workgroup scope, 2 u32 atomic agent,
+// 3 u32 atomic workgroup, 4 f32 workgroup scope into a per-XCD private copy,
+// 5 u32 workgroup into per-XCD copy, 6 plain store (rate reference),
+// 7 pk_add_f16 agent
+// SEGS: distinct 64-B segments per wave instruction (64/SEGS lanes each)
+template <int VAR>
+__global__ void __launch_bounds__(256) k_probe(float* buf, uint32_t nseg, int iters, int segs) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = (blockIdx.x * 4 + (threadIdx.x >> 6));
+    const int lanes_per_seg = 64 / segs;
+    const int sidx = lane / lanes_per_seg, within = lane % lanes_per_seg;
+    float* base = buf;
+    if (VAR == 4 || VAR == 5) {
+        base = buf + (size_t)xcc_id() * nseg * 16;
+    }
+    for (int i = 0; i < iters; ++i) {
+        const uint32_t seg = hash32(wave * 1315423911u + i * 64 + sidx) % nseg;
+        const size_t off = (size_t)seg * 16 + within;
+        const float v = 1.0f;
+        if (VAR == 0) {
+            __hip_atomic_fetch_add(base + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 1 || VAR == 4) {
+            __hip_atomic_fetch_add(base + off, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (VAR == 2) {
+            __hip_atomic_fetch_add((uint32_t*)(base + off), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 3 || VAR == 5) {
+            __hip_atomic_fetch_add((uint32_t*)(base + off), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else if (VAR == 6) {
+            base[off] = v + (float)i;
+        } else if (VAR == 8) {
+            // 8 B per lane: lanes_per_seg / 2 lanes cover one 64-B segment
+            unsigned long long* p = (unsigned long long*)base + (size_t)seg * 8 + (within & 7);
+            __hip_atomic_fetch_add(p, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 9) {
+            double* p = (double*)base + (size_t)seg * 8 + (within & 7);
+            __hip_atomic_fetch_add(p, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 7) {
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            h2 hv = {(_Float16)1.0f, (_Float16)1.0f};
+            __builtin_amdgcn_global_atomic_fadd_v2f16((h2*)(base + off), hv);
+        }
+    }
+}
+
+template <int VAR>
+static int run(float* buf, uint32_t nseg, int iters, int segs, const char* name) {
+    const int blocks = 256 * 8;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+    hipLaunchKernelGGL(k_probe<VAR>, dim3(blocks), dim3(256), 0, 0, buf, nseg, iters, segs);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(e0));
+    const int reps = 3;
+    for (int r = 0; r < reps; ++r)
+        hipLaunchKernelGGL(k_probe<VAR>, dim3(blocks), dim3(256), 0, 0, buf, nseg, iters, segs);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipGetLastError());
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    ms /= reps;
+    const double instr = (double)blocks * 4 * iters;
+    const double reqs = instr * segs;
+    printf("{\"variant\": \"%s\", \"segs_per_instr\": %d, \"ms\": %.4f, \"G_instr_s\": %.3f, "
+           "\"G_req64_s\": %.3f, \"payload_TB_s\": %.3f}\n",
+           name, segs, ms, instr / ms / 1e6, reqs / ms / 1e6, instr * 256.0 / ms / 1e9);
+    return 0;
+}
+
+int main() {
+    const uint32_t nseg = 45700000u / 64u;              // 45.7 MB table of 64-B segments
+    float* buf = nullptr;
+    CHECK(hipMalloc(&buf, (size_t)nseg * 64 * 8));      // room for 8 XCD-private copies
+    CHECK(hipMemset(buf, 0, (size_t)nseg * 64 * 8));
+    const int iters = 256;
+    for (int segs : {4, 16}) {
+        if (run<0>(buf, nseg, iters, segs, "f32_agent")) return 1;
+        if (run<1>(buf, nseg, iters, segs, "f32_workgroup")) return 1;
+        if (run<2>(buf, nseg, iters, segs, "u32_agent")) return 1;
+        if (run<3>(buf, nseg, iters, segs, "u32_workgroup")) return 1;
+        if (run<4>(buf, nseg, iters, segs, "f32_workgroup_xcd_private")) return 1;
+        if (run<5>(buf, nseg, iters, segs, "u32_workgroup_xcd_private")) return 1;
+        if (run<6>(buf, nseg, iters, segs, "plain_store")) return 1;
+        if (run<7>(buf, nseg, iters, segs, "pk_f16_agent")) return 1;
+    }
+    // 8-B lanes: segs_per_instr counts 64-B segments (8 lanes each at segs=8)
+    for (int segs : {8, 16}) {
+        if (run<8>(buf, nseg, iters, segs, "u64_agent_8B_lanes")) return 1;
+        if (run<9>(buf, nseg, iters, segs, "f64_agent_8B_lanes")) return 1;
+        if (run<2>(buf, nseg, iters, segs, "u32_agent")) return 1;
+    }
+    // small L2-resident footprint (256 KB per XCD copy)
+    for (int segs : {4}) {
+        if (run<4>(buf, 4096, iters, segs, "f32_workgroup_xcd_private_256KB")) return 1;
+        if (run<5>(buf, 4096, iters, segs, "u32_workgroup_xcd_private_256KB")) return 1;
+        if (run<3>(buf, 4096, iters, segs, "u32_workgroup_256KB")) return 1;
+    }
+    CHECK(hipFree(buf));
+    return 0;
+}
