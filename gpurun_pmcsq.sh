@@ -1,0 +1,6 @@
+#!/bin/bash
+set -u
+mkdir -p gpurun_out
+TAG=${1:-s}
+export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU -d gpurun_out/pmcsq_$TAG -o run --output-format csv -- python3 tools/ablate.py 0 4 32 > gpurun_out/pmcsq_$TAG.log 2>&1

@@ -128,7 +128,8 @@ __device__ __forceinline__ LvConst lv_const(const LvTab& T, const GridMeta& gm, 
 // index < res^3 + res^2 + res < 2*hsize, so `% hsize` is one conditional
 // subtract; hashed levels have hsize = 2^log2_T, so it is a mask.
 __device__ __forceinline__ uint32_t grid_index(const LvConst& c, uint32_t x, uint32_t y, uint32_t z) {
-    const uint32_t di = x + y * c.res + z * c.res2;
+    // dense levels: res <= 128 (res^3 <= hsize), so u24 multiplies are exact
+    const uint32_t di = x + __umul24(y, c.res) + __umul24(z, c.res2);
     const uint32_t hi = x ^ (y * 2654435761u) ^ (z * 805459861u);
     const uint32_t dm = di >= c.hs ? di - c.hs : di;
     return c.dense ? dm : (hi & (c.hs - 1u));
@@ -448,8 +449,8 @@ k_field_fwd(FieldArgs a) {
 // is a 4-B word.
 struct ScatterRing {
     uint32_t* ring;          // this wave's SC_STREAMS x 3 x SC_RING words
-    uint32_t head[SC_STREAMS];   // per stream, wave-uniform (monotonic counters)
-    uint32_t tail;           // per lane: the tail of this lane's stream
+    uint32_t head[SC_STREAMS];   // per stream, wave-uniform, in [0, SC_RING)
+    uint32_t tail;           // per lane: the tail of this lane's stream, in [0, SC_RING)
 };
 
 __device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
@@ -457,7 +458,8 @@ __device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
     const int lane = rn_lane();
     asm volatile("" ::: "memory");
     if ((uint32_t)lane < 2u * cnt) {
-        const uint32_t rec = (R.head[s] + (lane >> 1)) % SC_RING;
+        uint32_t rec = R.head[s] + (lane >> 1);          // < 2 SC_RING: no modulo
+        rec = rec >= SC_RING ? rec - SC_RING : rec;
         const uint32_t* base = R.ring + s * 3 * SC_RING;
         const uint32_t off = base[rec] + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * SC_RING + rec];
@@ -466,7 +468,8 @@ __device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
                                                              (int)off, 0, 0);
     }
     asm volatile("" ::: "memory");
-    R.head[s] += cnt;
+    const uint32_t h = R.head[s] + cnt;
+    R.head[s] = h >= SC_RING ? h - SC_RING : h;
 }
 
 // append this step's finished runs (lanes with `emit`) to their stream rings;
@@ -479,12 +482,14 @@ __device__ __forceinline__ void ring_push(ScatterRing& R, bool emit, uint64_t sm
     const int s = rn_lane() >> 3;
     if (emit) {
         uint32_t* base = R.ring + s * 3 * SC_RING;
-        const uint32_t rec = (R.tail + rank) % SC_RING;
+        uint32_t rec = R.tail + rank;
+        rec = rec >= SC_RING ? rec - SC_RING : rec;
         base[rec] = off;
         base[SC_RING + rec] = __float_as_uint(v0);
         base[2 * SC_RING + rec] = __float_as_uint(v1);
     }
-    R.tail += (uint32_t)(__builtin_popcount(lo) + __builtin_popcount(hi));
+    const uint32_t t = R.tail + (uint32_t)(__builtin_popcount(lo) + __builtin_popcount(hi));
+    R.tail = t >= SC_RING ? t - SC_RING : t;
 }
 
 __device__ __forceinline__ void ring_drain(ScatterRing& R, uint32_t min_cnt,
@@ -492,9 +497,95 @@ __device__ __forceinline__ void ring_drain(ScatterRing& R, uint32_t min_cnt,
 #pragma unroll
     for (int q = 0; q < SC_STREAMS; ++q) {
         const uint32_t t = __builtin_amdgcn_readlane(R.tail, 8 * q);
-        const uint32_t pend = t - R.head[q];
+        const uint32_t pend = t >= R.head[q] ? t - R.head[q] : t + SC_RING - R.head[q];
         if (pend >= min_cnt && pend > 0u) ring_issue(R, q, pend < 32u ? pend : 32u, grad_rs, dbg);
     }
+}
+
+// Walk state of one lane: its entry (coords, index) and the two features'
+// accumulated gradient.  Carried across windows by the merged kernel.
+struct WalkState {
+    uint32_t ex, ey, ez, cur;
+    float acc0, acc1;
+};
+
+__device__ __forceinline__ void walk_begin(WalkState& W) {
+    W.ex = 0xffffffffu; W.ey = 0; W.ez = 0; W.cur = 0; W.acc0 = 0.f; W.acc1 = 0.f;
+}
+
+__device__ __forceinline__ LvConst walk_level(const FieldArgs& a, const LvTab& sT) {
+    const int lane = rn_lane();
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+    const int l = ((lane >> 3) & 1) ? (RN_L - 1 - wid) : wid;
+    return lv_const(sT, a.gm, l);
+}
+
+// Walk one window of staged rows.  Stream quarter q's samples are rows
+// [64q, 64q + nq) of sG/sU (nq per lane: its quarter's count); n0 = the
+// largest nq (wave-uniform trip count).
+typedef __attribute__((address_space(3))) const float lds_cf;
+
+__device__ __forceinline__ void grid_walk_window(const FieldArgs& a, const LvTab& sT,
+                                                 const float* sG_, const float* sU_, int nq, int n0,
+                                                 ScatterRing& R, __amdgpu_buffer_rsrc_t grad_rs,
+                                                 WalkState& W, int dbg) {
+    // 32-bit LDS addressing (generic pointers make the row offsets 64-bit)
+    lds_cf* sG = (lds_cf*)sG_;
+    lds_cf* sU = (lds_cf*)sU_;
+    const int lane = rn_lane();
+    const int stream = lane >> 3, quarter = stream >> 1, par = lane & 7;
+    const uint32_t px = par & 1, py = (par >> 1) & 1, pz = par >> 2;
+    const LvConst lc = walk_level(a, sT);
+    const uint64_t smask = 0xffull << (8 * stream);
+    constexpr int QN = BWD_WAVES * 8;                     // rows per quarter
+    const int s_base = quarter * QN;
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+    lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - wid) : wid);
+    typedef float vf4 __attribute__((ext_vector_type(4)));
+    typedef float vf2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const vf4 lds_cf4;
+    typedef __attribute__((address_space(3))) const vf2 lds_cf2;
+    // software pipeline: this step's sample row is loaded one step ahead
+    vf4 un = *(lds_cf4*)(sU + s_base * 4);
+    vf2 gn = *(lds_cf2*)(gcol + s_base * SG_STRIDE);
+    for (int j0 = 0; j0 < n0; j0 += 2) {                  // wave-uniform trip count
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj) {
+            const int j = j0 + jj;
+            const bool act = j < nq;
+            const vf4 uc = un;
+            const vf2 gc = gn;
+            const int nx = s_base + (j + 1 < nq ? j + 1 : 0);
+            un = *(lds_cf4*)(sU + nx * 4);
+            gn = *(lds_cf2*)(gcol + nx * SG_STRIDE);
+            const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
+            // this class's corner of the cell: the one of {g, g+1} with parity p
+            const uint32_t cx = (px ^ p.gx) & 1u, cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
+            const uint32_t X = p.gx + cx, Y = p.gy + cy, Z = p.gz + cz;
+            const float w = (cx ? p.fx : 1.0f - p.fx) * (cy ? p.fy : 1.0f - p.fy) *
+                            (cz ? p.fz : 1.0f - p.fz);
+            const bool same = X == W.ex && Y == W.ey && Z == W.ez;
+            ring_push(R, act && !same && W.ex != 0xffffffffu, smask, 8u * (lc.off + W.cur),
+                      W.acc0, W.acc1);
+            if (act) {
+                W.acc0 = (same ? W.acc0 : 0.f) + w * gc.x;
+                W.acc1 = (same ? W.acc1 : 0.f) + w * gc.y;
+                W.cur = grid_index(lc, X, Y, Z);
+                W.ex = X; W.ey = Y; W.ez = Z;
+            }
+        }
+        ring_drain(R, 32u, grad_rs, dbg);
+    }
+}
+
+// end of a walk: emit the live entry of every lane
+__device__ __forceinline__ void walk_end(const FieldArgs& a, const LvTab& sT, ScatterRing& R,
+                                         __amdgpu_buffer_rsrc_t grad_rs, WalkState& W, int dbg) {
+    const LvConst lc = walk_level(a, sT);
+    const uint64_t smask = 0xffull << (8 * (rn_lane() >> 3));
+    ring_push(R, W.ex != 0xffffffffu, smask, 8u * (lc.off + W.cur), W.acc0, W.acc1);
+    ring_drain(R, 32u, grad_rs, dbg);
+    walk_begin(W);
 }
 
 // Walk of one wave over the block's 256 samples.  Lane = (stream, parity
@@ -509,54 +600,14 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
                                                    const float* sG, const float* sU, int nblk,
                                                    ScatterRing& R,
                                                    __amdgpu_buffer_rsrc_t grad_rs) {
-    const int lane = rn_lane();
-    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-    const int stream = lane >> 3, quarter = stream >> 1, par = lane & 7;
-    const uint32_t px = par & 1, py = (par >> 1) & 1, pz = par >> 2;
-    const int l = (stream & 1) ? (RN_L - 1 - wid) : wid;
-    const LvConst lc = lv_const(sT, a.gm, l);
-    const uint64_t smask = 0xffull << (8 * stream);
-    constexpr int QN = BWD_WAVES * 8;                     // samples per quarter
+    constexpr int QN = BWD_WAVES * 8;
+    const int quarter = rn_lane() >> 4;
     const int n0 = min(nblk, QN);                         // quarter 0 is the longest
     const int nq = max(0, min(QN, nblk - quarter * QN));
-    const int s_base = quarter * QN;
-    const float* gcol = sG + 2 * l;
-    uint32_t ex = 0xffffffffu, ey = 0, ez = 0;            // current entry coords (none yet)
-    uint32_t cur = 0;
-    float acc0 = 0.f, acc1 = 0.f;
-    // software pipeline: this step's sample row is loaded one step ahead
-    float4 un = *reinterpret_cast<const float4*>(sU + s_base * 4);
-    float2 gn = *reinterpret_cast<const float2*>(gcol + s_base * SG_STRIDE);
-    for (int j0 = 0; j0 < n0; j0 += 2) {                  // wave-uniform trip count
-#pragma unroll
-        for (int jj = 0; jj < 2; ++jj) {
-            const int j = j0 + jj;
-            const bool act = j < nq;
-            const float4 uc = un;
-            const float2 gc = gn;
-            const int nx = s_base + (j + 1 < nq ? j + 1 : 0);
-            un = *reinterpret_cast<const float4*>(sU + nx * 4);
-            gn = *reinterpret_cast<const float2*>(gcol + nx * SG_STRIDE);
-            const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
-            // this class's corner of the cell: the one of {g, g+1} with parity p
-            const uint32_t cx = (px ^ p.gx) & 1u, cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
-            const uint32_t X = p.gx + cx, Y = p.gy + cy, Z = p.gz + cz;
-            const float w = (cx ? p.fx : 1.0f - p.fx) * (cy ? p.fy : 1.0f - p.fy) *
-                            (cz ? p.fz : 1.0f - p.fz);
-            const bool same = X == ex && Y == ey && Z == ez;
-            ring_push(R, act && !same && ex != 0xffffffffu, smask, 8u * (lc.off + cur), acc0,
-                      acc1);
-            if (act) {
-                acc0 = (same ? acc0 : 0.f) + w * gc.x;
-                acc1 = (same ? acc1 : 0.f) + w * gc.y;
-                cur = grid_index(lc, X, Y, Z);
-                ex = X; ey = Y; ez = Z;
-            }
-        }
-        ring_drain(R, 32u, grad_rs, a.dbg);
-    }
-    ring_push(R, ex != 0xffffffffu, smask, 8u * (lc.off + cur), acc0, acc1);
-    ring_drain(R, 32u, grad_rs, a.dbg);
+    WalkState W;
+    walk_begin(W);
+    grid_walk_window(a, sT, sG, sU, nq, n0, R, grad_rs, W, a.dbg);
+    walk_end(a, sT, R, grad_rs, W, a.dbg);
 }
 
 // dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
@@ -866,7 +917,7 @@ __device__ __forceinline__ void dw_unpark(const float* p, f32x16& A, f32x16& B) 
     }
 }
 
-template <int CACHE>
+template <int CACHE, bool ABL>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
 k_field_bwd_merged(FieldArgs a, MergeArgs m) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
@@ -886,8 +937,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
     rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
     rn_half* imgX = imgY + RN_IMG_HALFS;
     const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
-    const bool do_dw = !(a.dbg & 2);
-    const bool do_sc = !(a.dbg & 4);
+    const int dbg = ABL ? a.dbg : 0;      // ablation flags (tools/ablate.py) only in ABL builds
+    const bool do_dw = !(dbg & 2);
+    const bool do_sc = !(dbg & 4);
     float* sG = reinterpret_cast<float*>(sImg);
     float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;
     ScatterRing R;
@@ -983,15 +1035,23 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
         // ---- 2. scatter in merged (ray, t) order
         __builtin_amdgcn_s_waitcnt(0x0070);     // vmcnt(0): this wave's rows are in L2
         __syncthreads();
+        // the chunk's merged order is cut into 4 contiguous quarters, one per
+        // stream quarter; each window stages the next 64 rows of every quarter
+        // and the walks carry their state across windows (no restart per window)
         const int p_base = m.mstart[r0], n_p = m.mstart[r1] - p_base;
-        for (int p0 = 0; p0 < n_p; p0 += BWD_WAVES * 32) {
-            const int nblk = min(BWD_WAVES * 32, n_p - p0);
+        const int Q = (n_p + 3) >> 2;
+        const int qlen_lane = max(0, min(Q, n_p - (rn_lane() >> 4) * Q));   // walk quarter
+        WalkState W;
+        walk_begin(W);
+        for (int w0 = 0; w0 < Q; w0 += 64) {
             const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
+            const int q = j >> 6, jj = j & 63;
+            const int qlen = max(0, min(Q, n_p - q * Q));
             int nz = 0;
-            if (j < nblk) {
-                const int smp = m.perm[p_base + p0 + j];
+            if (w0 + jj < qlen) {
+                const int smp = m.perm[p_base + q * Q + w0 + jj];
                 int k = 0;
-                for (int q = 1; q < K; ++q) k = smp >= sCh[2 + 3 * MB_KMAX + q] ? q : k;
+                for (int kq = 1; kq < K; ++kq) k = smp >= sCh[2 + 3 * MB_KMAX + kq] ? kq : k;
                 const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
                 // rows were written by other waves of this block: read past L1 (nt)
                 typedef float nf4 __attribute__((ext_vector_type(4)));
@@ -999,10 +1059,10 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
                                  + 4 * half;
                 float* dst = sG + j * SG_STRIDE + 16 * half;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const nf4 v = __builtin_nontemporal_load(src + q);
-                    *reinterpret_cast<float2*>(dst + 4 * q) = make_float2(v.x, v.y);
-                    *reinterpret_cast<float2*>(dst + 4 * q + 2) = make_float2(v.z, v.w);
+                for (int qq = 0; qq < 4; ++qq) {
+                    const nf4 v = __builtin_nontemporal_load(src + qq);
+                    *reinterpret_cast<float2*>(dst + 4 * qq) = make_float2(v.x, v.y);
+                    *reinterpret_cast<float2*>(dst + 4 * qq + 2) = make_float2(v.z, v.w);
                     nz |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
                 }
                 if (half) {
@@ -1012,12 +1072,18 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
                 }
             }
             // a window whose rows are all zero (rays past early termination)
-            // adds nothing to the grid
-            if (__syncthreads_or(nz)) grid_scatter_block(a, sT, sG, sU, nblk, R, grad_rs);
+            // adds nothing; skipping it keeps the walk state valid (entries
+            // are identified by their coordinates)
+            if (__syncthreads_or(nz) && !(dbg & 32)) {
+                const int nq = max(0, min(64, qlen_lane - w0));
+                const int n0 = max(0, min(64, min(Q, n_p) - w0));
+                grid_walk_window(a, sT, sG, sU, nq, n0, R, grad_rs, W, dbg);
+            }
             __syncthreads();
         }
+        walk_end(a, sT, R, grad_rs, W, dbg);
     }
-    if (do_sc) ring_drain(R, 0u, grad_rs, a.dbg);
+    if (do_sc) ring_drain(R, 0u, grad_rs, dbg);
     // ---- flush every model's dW (the current one from registers)
     if (do_dw) {
         for (int k = 0; k < K; ++k) {
@@ -1287,10 +1353,14 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     m.queue = queue;
     m.scratch = scratch; m.park = park;
     m.n_rays = (int)n_rays; m.n_models = n_models; m.rows_cap = (int)scratch_rows;
-    if (feat_cache)
-        k_field_bwd_merged<CACHE_READ><<<blocks, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a, m);
-    else
-        k_field_bwd_merged<CACHE_NONE><<<blocks, BWD_WAVES * 64, 0, (hipStream_t)stream>>>(a, m);
+    hipStream_t st = (hipStream_t)stream;
+    if (a.dbg) {
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+        else k_field_bwd_merged<CACHE_NONE, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+    } else {
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+        else k_field_bwd_merged<CACHE_NONE, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+    }
     RN_CHECK_LAUNCH();
     return 0;
 }
