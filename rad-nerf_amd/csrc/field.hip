@@ -588,6 +588,177 @@ __device__ __forceinline__ void walk_end(const FieldArgs& a, const LvTab& sT, Sc
     walk_begin(W);
 }
 
+// ---------------------------------------------------------------------------
+// Row-lane walk of the merged kernel.  Lane = (stream, yz parity class):
+// 16 streams per wave = (eighth of the chunk's merged order, level w or
+// 15-w), 4 lanes per stream.  A lane tracks the two corners of the current
+// cell in its (Y, Z) row (every cell has one corner per parity class
+// (X&1, Y&1, Z&1); the lane's row holds the even-X and the odd-X one), so the
+// per-sample position, the y/z weights and the row's hash part are computed
+// once for two entries (the 8-lane form above computes them per corner).
+// Finished entries go to per-stream LDS rings (SoA, W2_RING records) and are
+// issued 32 at a time: one instruction = one level of one stretch of rays.
+// The rings live in LDS that the MLP phase reuses, so every chunk ends with a
+// full drain (walk2_end).
+// ---------------------------------------------------------------------------
+#define W2_STREAMS 16
+#define W2_RING 40          // >= 31 pending + 8 pushed per step
+#define W2_RING_WORDS (W2_STREAMS * 3 * W2_RING)   // per wave
+#define W2_NONE 0xffffffffu
+
+struct Walk2 {
+    uint32_t* ring;        // this wave's rings: [stream][3][W2_RING] words
+    uint32_t head, tail;   // per lane: its stream's ring head / tail, in [0, W2_RING)
+    uint32_t ex0, ex1, ey, ez, cur0, cur1;   // even-X / odd-X entries of the row
+    float a00, a01, a10, a11;                // their accumulated feature gradients
+};
+
+__device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
+    W.ring = ring; W.head = 0; W.tail = 0;
+    W.ex0 = W2_NONE; W.ex1 = W2_NONE; W.ey = 0; W.ez = 0; W.cur0 = 0; W.cur1 = 0;
+    W.a00 = W.a01 = W.a10 = W.a11 = 0.f;
+}
+
+__device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? v - W2_RING : v; }
+
+// issue up to 32 records of stream s (wave-uniform) as one atomic instruction
+__device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
+                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+    const int lane = rn_lane();
+    const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
+    asm volatile("" ::: "memory");
+    if ((uint32_t)lane < 2u * cnt) {
+        const uint32_t rec = w2_wrap(h + (lane >> 1));
+        const uint32_t* base = W.ring + s * 3 * W2_RING;
+        const uint32_t off = base[rec] + 4u * (lane & 1);
+        const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
+        if (dbg & 1) asm volatile("" :: "v"(off), "v"(v));
+        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
+                                                             (int)off, 0, 0);
+    }
+    asm volatile("" ::: "memory");
+    if ((lane >> 2) == s) W.head = w2_wrap(W.head + cnt);
+}
+
+// issue every stream with >= min_cnt pending (min_cnt 0: drain all)
+__device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
+                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+    const bool lead = (rn_lane() & 3) == 0;
+    for (;;) {
+        const uint32_t pend = W.tail >= W.head ? W.tail - W.head : W.tail + W2_RING - W.head;
+        uint64_t m = __builtin_amdgcn_ballot_w64(lead && pend > 0u && pend >= min_cnt);
+        if (!m) break;
+        while (m) {
+            const int s = __builtin_ctzll(m) >> 2;
+            const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
+            walk2_issue(W, s, p < 32u ? p : 32u, grad_rs, dbg);
+            m &= m - 1;
+        }
+        if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
+    }
+}
+
+// append this step's finished entries (up to 2 per lane) to the stream rings
+__device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint64_t smask,
+                                           uint32_t lvl_off) {
+    const uint64_t m0 = __builtin_amdgcn_ballot_w64(e0) & smask;
+    const uint64_t m1 = __builtin_amdgcn_ballot_w64(e1) & smask;
+    const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
+    const int s = rn_lane() >> 2;
+    uint32_t* base = W.ring + s * 3 * W2_RING;
+    if (e0) {
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
+        const uint32_t rec = w2_wrap(W.tail + r);
+        base[rec] = 8u * (lvl_off + W.cur0);
+        base[W2_RING + rec] = __float_as_uint(W.a00);
+        base[2 * W2_RING + rec] = __float_as_uint(W.a01);
+    }
+    if (e1) {
+        const uint32_t r = n0 + __builtin_amdgcn_mbcnt_hi(
+                                    (uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
+        const uint32_t rec = w2_wrap(W.tail + r);
+        base[rec] = 8u * (lvl_off + W.cur1);
+        base[W2_RING + rec] = __float_as_uint(W.a10);
+        base[2 * W2_RING + rec] = __float_as_uint(W.a11);
+    }
+    W.tail = w2_wrap(W.tail + n0 + (uint32_t)__builtin_popcountll(m1));
+}
+
+__device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& sT) {
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+    const int l = ((rn_lane() >> 2) & 1) ? (RN_L - 1 - wid) : wid;
+    return lv_const(sT, a.gm, l);
+}
+
+// walk one window: eighth e's samples are rows [32e, 32e + ne) of sG/sU
+// (ne per lane: its eighth's count; n0 = the largest, wave-uniform)
+__device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT,
+                                             const float* sG_, const float* sU_, int ne, int n0,
+                                             __amdgpu_buffer_rsrc_t grad_rs, Walk2& W, int dbg) {
+    lds_cf* sG = (lds_cf*)sG_;
+    lds_cf* sU = (lds_cf*)sU_;
+    const int lane = rn_lane();
+    const int stream = lane >> 2, eighth = stream >> 1;
+    const uint32_t py = lane & 1, pz = (lane >> 1) & 1;
+    const LvConst lc = walk2_level(a, sT);
+    const uint64_t smask = 0xfull << (4 * stream);
+    const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+    lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - wid) : wid);
+    const int s_base = eighth * 32;
+    typedef float vf4 __attribute__((ext_vector_type(4)));
+    typedef float vf2 __attribute__((ext_vector_type(2)));
+    typedef __attribute__((address_space(3))) const vf4 lds_cf4;
+    typedef __attribute__((address_space(3))) const vf2 lds_cf2;
+    vf4 un = *(lds_cf4*)(sU + s_base * 4);
+    vf2 gn = *(lds_cf2*)(gcol + s_base * SG_STRIDE);
+    for (int j = 0; j < n0; ++j) {                        // wave-uniform trip count
+        const bool act = j < ne;
+        const vf4 uc = un;
+        const vf2 gc = gn;
+        const int nx = s_base + (j + 1 < ne ? j + 1 : 0);
+        un = *(lds_cf4*)(sU + nx * 4);
+        gn = *(lds_cf2*)(gcol + nx * SG_STRIDE);
+        const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
+        const uint32_t c0 = p.gx & 1u;                    // x offset of the even-X corner
+        const uint32_t cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
+        const uint32_t X0 = p.gx + c0, X1 = p.gx + (c0 ^ 1u), Y = p.gy + cy, Z = p.gz + cz;
+        const float fxm = 1.0f - p.fx;
+        const float wy = cy ? p.fy : 1.0f - p.fy, wz = cz ? p.fz : 1.0f - p.fz;
+        // weight = wx * wy * wz in tcnn's dimension order
+        const float w0 = ((c0 ? p.fx : fxm) * wy) * wz;
+        const float w1 = ((c0 ? fxm : p.fx) * wy) * wz;
+        const bool row = Y == W.ey && Z == W.ez;
+        const bool same0 = row && X0 == W.ex0, same1 = row && X1 == W.ex1;
+        walk2_push(W, act && !same0 && W.ex0 != W2_NONE, act && !same1 && W.ex1 != W2_NONE,
+                   smask, lc.off);
+        if (act) {
+            W.a00 = (same0 ? W.a00 : 0.f) + w0 * gc.x;
+            W.a01 = (same0 ? W.a01 : 0.f) + w0 * gc.y;
+            W.a10 = (same1 ? W.a10 : 0.f) + w1 * gc.x;
+            W.a11 = (same1 ? W.a11 : 0.f) + w1 * gc.y;
+            // tcnn grid_index with the row part shared by the two entries
+            const uint32_t db = __umul24(Y, lc.res) + __umul24(Z, lc.res2);
+            const uint32_t hb = (Y * 2654435761u) ^ (Z * 805459861u);
+            const uint32_t d0 = X0 + db, d1 = X1 + db;
+            W.cur0 = lc.dense ? (d0 >= lc.hs ? d0 - lc.hs : d0) : ((X0 ^ hb) & (lc.hs - 1u));
+            W.cur1 = lc.dense ? (d1 >= lc.hs ? d1 - lc.hs : d1) : ((X1 ^ hb) & (lc.hs - 1u));
+            W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
+        }
+        walk2_drain(W, 32u, grad_rs, dbg);
+    }
+}
+
+// end of a chunk: emit every live entry and drain the rings completely
+__device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
+                                          __amdgpu_buffer_rsrc_t grad_rs, Walk2& W, int dbg) {
+    const LvConst lc = walk2_level(a, sT);
+    const uint64_t smask = 0xfull << (4 * (rn_lane() >> 2));
+    walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, smask, lc.off);
+    walk2_drain(W, 0u, grad_rs, dbg);
+    walk2_begin(W, W.ring);
+}
+
 // Walk of one wave over the block's 256 samples.  Lane = (stream, parity
 // class): stream = (quarter of the samples, level w or 15-w), and each of the
 // stream's 8 lanes tracks the current cell's corner of one parity class
@@ -942,11 +1113,14 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
     const bool do_sc = !(dbg & 4);
     float* sG = reinterpret_cast<float*>(sImg);
     float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;
-    ScatterRing R;
-    R.ring = sRing + wid * SC_STREAMS * 3 * SC_RING;
-#pragma unroll
-    for (int q = 0; q < SC_STREAMS; ++q) R.head[q] = 0;
-    R.tail = 0;
+    // walk rings: waves 0-3 in sRing, waves 4-7 in the image region past the
+    // scatter staging (free during the scatter phase; drained every chunk)
+    static_assert(4 * W2_RING_WORDS * 4 <= BWD_WAVES * SC_STREAMS * 3 * SC_RING * 4, "rings");
+    static_assert(BWD_WAVES * 32 * (SG_STRIDE + 4) * 4 + 4 * W2_RING_WORDS * 4 <=
+                  BWD_WAVES * 2 * RN_IMG_HALFS * 2, "rings in the image region");
+    uint32_t* ring2 = wid < 4 ? sRing + wid * W2_RING_WORDS
+                              : reinterpret_cast<uint32_t*>(sU + BWD_WAVES * 32 * 4) +
+                                    (wid - 4) * W2_RING_WORDS;
 
     f32x16 accA = rn_zero16(), accB = rn_zero16();
     float cur_scale = 0.f;
@@ -1035,21 +1209,21 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
         // ---- 2. scatter in merged (ray, t) order
         __builtin_amdgcn_s_waitcnt(0x0070);     // vmcnt(0): this wave's rows are in L2
         __syncthreads();
-        // the chunk's merged order is cut into 4 contiguous quarters, one per
-        // stream quarter; each window stages the next 64 rows of every quarter
+        // the chunk's merged order is cut into 8 contiguous eighths, one per
+        // stream eighth; each window stages the next 32 rows of every eighth
         // and the walks carry their state across windows (no restart per window)
         const int p_base = m.mstart[r0], n_p = m.mstart[r1] - p_base;
-        const int Q = (n_p + 3) >> 2;
-        const int qlen_lane = max(0, min(Q, n_p - (rn_lane() >> 4) * Q));   // walk quarter
-        WalkState W;
-        walk_begin(W);
-        for (int w0 = 0; w0 < Q; w0 += 64) {
+        const int E = (n_p + 7) >> 3;
+        const int elen_lane = max(0, min(E, n_p - (rn_lane() >> 3) * E));   // walk eighth
+        Walk2 W;
+        walk2_begin(W, ring2);
+        for (int w0 = 0; w0 < E; w0 += 32) {
             const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
-            const int q = j >> 6, jj = j & 63;
-            const int qlen = max(0, min(Q, n_p - q * Q));
+            const int e = j >> 5, jj = j & 31;
+            const int elen = max(0, min(E, n_p - e * E));
             int nz = 0;
-            if (w0 + jj < qlen) {
-                const int smp = m.perm[p_base + q * Q + w0 + jj];
+            if (w0 + jj < elen) {
+                const int smp = m.perm[p_base + e * E + w0 + jj];
                 int k = 0;
                 for (int kq = 1; kq < K; ++kq) k = smp >= sCh[2 + 3 * MB_KMAX + kq] ? kq : k;
                 const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
@@ -1075,15 +1249,15 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
             // adds nothing; skipping it keeps the walk state valid (entries
             // are identified by their coordinates)
             if (__syncthreads_or(nz) && !(dbg & 32)) {
-                const int nq = max(0, min(64, qlen_lane - w0));
-                const int n0 = max(0, min(64, min(Q, n_p) - w0));
-                grid_walk_window(a, sT, sG, sU, nq, n0, R, grad_rs, W, dbg);
+                const int ne = max(0, min(32, elen_lane - w0));
+                const int n0 = max(0, min(32, min(E, n_p) - w0));
+                walk2_window(a, sT, sG, sU, ne, n0, grad_rs, W, dbg);
             }
             __syncthreads();
         }
-        walk_end(a, sT, R, grad_rs, W, dbg);
+        walk2_end(a, sT, grad_rs, W, dbg);
+        __syncthreads();                         // rings (image region) drained
     }
-    if (do_sc) ring_drain(R, 0u, grad_rs, dbg);
     // ---- flush every model's dW (the current one from registers)
     if (do_dw) {
         for (int k = 0; k < K; ++k) {
