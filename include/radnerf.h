@@ -190,7 +190,7 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * rn_bwd_plan builds the merged order (mstart [n_rays + 1] i32, perm [total]
  * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: chunks of
  * max_chunk merged samples for the first 7/8 of the work, then min_chunk;
- * queue [2] i32 = ticket, chunk count).  cap_chunks must bound the chunk
+ * queue [3] i32 = bwd ticket, chunk count, fwd ticket).  cap_chunks must bound the chunk
  * count: >= total/max_chunk + total/(8*min_chunk) + 2.
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
  * stages 144-B rows in its scratch slice (scratch: blocks x scratch_rows x 36
@@ -214,6 +214,22 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const void* frags, const float* dL_dsigma, const float* dL_drgb,
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
+                        void* stream);
+
+/* Merged forward (fused training path, n_models <= 4): same outputs as
+ * rn_field_fwd in compact mode, but blocks take rn_bwd_plan's chunks (queue
+ * [2] is the forward's ticket) and evaluate the models' tiles of a chunk
+ * interleaved, so the K sub-NeRFs' samples of one ray share cached grid
+ * lines.  Replaces the per-sub-NeRF MNGP forward (models/networks.py:300-328
+ * via ml_rendering.py:174-179).                                            */
+int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        const int32_t* offsets, const int32_t* chunk_first, int32_t* queue,
+                        int64_t n_rays, int32_t n_models, const void* grid_f16,
+                        const uint32_t* level_offset, const uint32_t* level_hsize,
+                        const uint32_t* level_res, const float* level_scale,
+                        const float* xyz_min, const float* extent, const void* frags,
+                        float* sigma, float* rgb, void* feat_cache, int32_t blocks,
                         void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------

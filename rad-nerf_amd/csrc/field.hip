@@ -337,7 +337,7 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
     } else {
         if (a.dbg & 256) { st.e0 = rn_zero8(); st.e1 = rn_zero8(); asm volatile("" :: "v"(ux), "v"(uy), "v"(uz)); }
         else encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
-        if (CACHE == CACHE_WRITE) { fc[0] = st.e0; fc[1] = st.e1; }
+        if (CACHE == CACHE_WRITE && valid) { fc[0] = st.e0; fc[1] = st.e1; }
     }
     st.sh = sh_lane(dx, dy, dz, h);
     mlp_forward(W, st);
@@ -1067,7 +1067,7 @@ struct MergeArgs {
     const int32_t* mstart;   // [B + 1] first merged position of ray r; [B] = total
     const int32_t* perm;     // [total] merged position -> sample index
     const int32_t* chunk_first;  // [n_chunks + 1] first ray of each chunk; [n] = B
-    int32_t* queue;          // [0] ticket counter, [1] n_chunks (rn_bwd_plan)
+    int32_t* queue;          // [0] bwd ticket, [1] n_chunks, [2] fwd ticket (rn_bwd_plan)
     float* scratch;          // [gridDim.x][rows_cap][MB_ROW]
     float* park;             // [gridDim.x][K][BWD_WAVES][32][64]
     int32_t n_rays, n_models, rows_cap;
@@ -1270,6 +1270,78 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Merged forward: blocks take the plan's chunks (whole rays) and evaluate the
+// K models' tiles of a chunk interleaved (tile i of model 0, tile i of model
+// 1, ...), so the models' samples of the same rays are gathered close in time
+// by the same CU: the second model's corners hit L1/L2 lines the first one
+// fetched (the fine levels otherwise miss L2 for every sample).  All K
+// models' forward fragments sit in LDS (dynamic, K x 24 KB; K <= 4).
+// Same outputs as k_field_fwd (per-sample arithmetic is identical).
+// ---------------------------------------------------------------------------
+#define FM_KMAX 4
+
+template <int CACHE>
+__global__ void __launch_bounds__(512)
+k_field_fwd_merged(FieldArgs a, MergeArgs m) {
+    extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
+    __shared__ LvTab sT;
+    __shared__ int32_t sCh[2 + 2 * FM_KMAX];
+    const int K = m.n_models, B = m.n_rays;
+    for (int k = 0; k < K; ++k)
+        rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
+                        a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
+                        FIELD_FWD_FRAGS * RN_FRAG_BYTES);
+    lv_stage(sT, a.gm);
+    const int waves = blockDim.x / RN_WAVE;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const int n_chunks = m.queue[1];
+            int r0 = B, r1 = B;
+            for (;;) {
+                const int ch = atomicAdd(m.queue + 2, 1);
+                if (ch >= n_chunks) break;
+                r0 = m.chunk_first[ch]; r1 = m.chunk_first[ch + 1];
+                if (r1 > r0) break;
+                r0 = B;
+            }
+            sCh[0] = r0;
+            for (int k = 0; k < K; ++k) {
+                const int a0 = r0 < B ? m.offsets[k * B + r0] : 0;
+                const int a1 = r1 < B ? m.offsets[k * B + r1] : a.seg_base[k] + a.seg_count[k];
+                sCh[2 + k] = a0; sCh[2 + FM_KMAX + k] = r0 < B ? a1 - a0 : 0;
+            }
+        }
+        __syncthreads();
+        if (sCh[0] >= B) break;
+        int max_t = 0;
+        for (int k = 0; k < K; ++k) max_t = max(max_t, (sCh[2 + FM_KMAX + k] + 31) >> 5);
+        for (int u = wid; u < max_t * K; u += waves) {
+            const int k = u % K, t = u / K;
+            const int n_k = sCh[2 + FM_KMAX + k];
+            if (t * 32 >= n_k) continue;                     // wave-uniform
+            rn_lds_order();
+            const int i = t * 32 + c;
+            const bool valid = i < n_k;
+            const int64_t s = sCh[2 + k] + (valid ? i : 0);
+            FwdState st;
+            float ux, uy, uz;
+            tile_forward_s<1, CACHE>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
+                                     valid, CACHE == CACHE_WRITE ? cache_slot(a, s) : nullptr,
+                                     st, ux, uy, uz);
+            if (valid && h == 0) {
+                a.sigma[s] = expf(st.g0);
+                a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
+                a.rgb[3 * s + 1] = (float)(rn_half)sigmoidf(st.out[1]);
+                a.rgb[3 * s + 2] = (float)(rn_half)sigmoidf(st.out[2]);
+            }
+        }
+    }
+}
+
 // Merged order of the K models' samples per ray (ray-major, then t, ties by
 // model): perm[mstart[r] + rank] = sample.  One wave per ray; each sample's
 // rank = its index in its (model, ray) run + the samples of the other models
@@ -1331,7 +1403,7 @@ k_bwd_chunks(int B, const int32_t* __restrict__ mstart, int max_chunk, int min_c
     const int total = mstart[B];
     int c1, n;
     chunk_plan(total, max_chunk, min_chunk, c1, n);
-    if (c == 0) { queue[0] = 0; queue[1] = n < cap_chunks ? n : cap_chunks; }
+    if (c == 0) { queue[0] = 0; queue[1] = n < cap_chunks ? n : cap_chunks; queue[2] = 0; }
     if (c > n || c > cap_chunks) return;
     if (c == n || c == cap_chunks) { chunk_first[c] = B; return; }
     const int bound = c <= c1 ? c * max_chunk : c1 * max_chunk + (c - c1) * min_chunk;
@@ -1528,6 +1600,11 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     m.scratch = scratch; m.park = park;
     m.n_rays = (int)n_rays; m.n_models = n_models; m.rows_cap = (int)scratch_rows;
     hipStream_t st = (hipStream_t)stream;
+    // the ticket is reset per launch, so a backward can be re-run on one plan
+    if (hipMemsetAsync(queue, 0, sizeof(int32_t), st) != hipSuccess) {
+        rn_set_error("%s: ticket reset failed", __func__);
+        return 2;
+    }
     if (a.dbg) {
         if (feat_cache) k_field_bwd_merged<CACHE_READ, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
         else k_field_bwd_merged<CACHE_NONE, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
@@ -1535,6 +1612,42 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         if (feat_cache) k_field_bwd_merged<CACHE_READ, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
         else k_field_bwd_merged<CACHE_NONE, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
     }
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        const int32_t* offsets, const int32_t* chunk_first, int32_t* queue,
+                        int64_t n_rays, int32_t n_models, const void* grid_f16,
+                        const uint32_t* level_offset, const uint32_t* level_hsize,
+                        const uint32_t* level_res, const float* level_scale,
+                        const float* xyz_min, const float* extent, const void* frags,
+                        float* sigma, float* rgb, void* feat_cache, int32_t blocks,
+                        void* stream) {
+    RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && blocks >= 1,
+                 "bad sizes (n_models <= 4)");
+    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets &&
+                 chunk_first && queue && grid_f16 && level_offset && level_hsize && level_res &&
+                 level_scale && xyz_min && extent && frags && sigma && rgb, "null pointer");
+    FieldArgs a{};
+    fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
+    a.dbg = g_field_dbg;
+    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
+    a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
+    a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
+    a.seg_base = seg_base; a.seg_count = seg_count;
+    MergeArgs m{};
+    m.offsets = offsets; m.chunk_first = chunk_first; m.queue = queue;
+    m.n_rays = (int)n_rays; m.n_models = n_models;
+    const size_t lds = (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(queue + 2, 0, sizeof(int32_t), st) != hipSuccess) {
+        rn_set_error("%s: ticket reset failed", __func__);
+        return 2;
+    }
+    if (feat_cache) k_field_fwd_merged<CACHE_WRITE><<<blocks, 512, lds, st>>>(a, m);
+    else k_field_fwd_merged<CACHE_NONE><<<blocks, 512, lds, st>>>(a, m);
     RN_CHECK_LAUNCH();
     return 0;
 }

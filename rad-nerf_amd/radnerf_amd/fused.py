@@ -61,7 +61,7 @@ class Workspace:
         # merged backward (rn_bwd_plan): per-ray merged starts, merged order, queue head
         self.mstart = torch.empty(B + 1, **i)
         self.perm = torch.empty(cap, **i)
-        self.queue = torch.zeros(2, **i)
+        self.queue = torch.zeros(3, **i)
         self._bwd_scratch = None
         self._chunks = None
 
@@ -116,6 +116,12 @@ class FusedMLRenderer:
         # backward scatters the K models' grid gradients merged per ray
         # (rn_field_bwd_merged); False: one model per block (rn_field_bwd)
         self.merged_bwd = True
+        # forward evaluating the K models' tiles of a chunk interleaved
+        # (rn_field_fwd_merged, K <= 4): bit-exact with rn_field_fwd and measured
+        # no faster (1.31 vs 1.30 ms on C3: the gathers are not L2-miss bound),
+        # so off by default
+        self.merged_fwd = False
+        self.merged_fwd_blocks = 512
         self.merged_blocks = 256
         self.max_chunk = 4096
         self.min_chunk = 512
@@ -184,6 +190,8 @@ class FusedMLRenderer:
         self._ev("compact", L.ml_compact, w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
                  MAX_SAMPLES, w.stage_ts.data_ptr(), w.stage_dt.data_ptr(), w.ts.data_ptr(),
                  w.deltas.data_ptr(), w.ray_of.data_ptr(), st)
+        if self.merged_bwd or self.merged_fwd:
+            self._plan(st)
         self._field(True, rays_o, rays_d, st)
         self._ev("composite_fw", L.ml_composite_fw, w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
                           w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
@@ -200,6 +208,18 @@ class FusedMLRenderer:
                         opacity.data_ptr(), depth.data_ptr(), st)
         return rgb, opacity, depth, out_gate, imp
 
+    def _plan(self, st):
+        """Merged (ray, t) order + chunk schedule of this step's samples
+        (rn_bwd_plan), shared by the merged forward and backward."""
+        w, L = self.ws, lib()
+        self._min_chunk = min(self.min_chunk, self.max_chunk)
+        self._cap_chunks, self._chunks = w.chunk_list(self.max_chunk, self._min_chunk)
+        self._ev("bwd_plan", L.bwd_plan, w.counts.data_ptr(), w.offsets.data_ptr(),
+                 w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, w.K,
+                 self.max_chunk, self._min_chunk, self._cap_chunks, w.mstart.data_ptr(),
+                 w.perm.data_ptr(), self._chunks.data_ptr(), w.queue.data_ptr(), st)
+        self._plan_key = (self.max_chunk, self._min_chunk)
+
     def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
         m, w, L = self.model, self.ws, lib()
         lo, lh, lr, ls = m.xyz_encoder.level_ptrs()
@@ -207,17 +227,22 @@ class FusedMLRenderer:
                   rays_d.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(), m.size,
                   m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
-        if fwd:
+        if fwd and self.merged_fwd:
+            self._ev("field_fwd", L.field_fwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
+                     rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
+                     w.seg_count.data_ptr(), w.offsets.data_ptr(), self._chunks.data_ptr(),
+                     w.queue.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
+                     w.rgb.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
+                     self.merged_fwd_blocks, st)
+        elif fwd:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
                      w.feat.data_ptr() if self.feat_cache else None, self.fwd_blocks, st)
         elif self.merged_bwd:
             rows, scratch, park = w.bwd_scratch(self.merged_blocks, self.max_chunk)
-            min_chunk = min(self.min_chunk, self.max_chunk)
-            cap, chunks = w.chunk_list(self.max_chunk, min_chunk)
-            self._ev("bwd_plan", L.bwd_plan, w.counts.data_ptr(), w.offsets.data_ptr(),
-                     w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, m.size,
-                     self.max_chunk, min_chunk, cap, w.mstart.data_ptr(), w.perm.data_ptr(),
-                     chunks.data_ptr(), w.queue.data_ptr(), st)
+            if getattr(self, "_plan_key", None) != (self.max_chunk,
+                                                    min(self.min_chunk, self.max_chunk)):
+                self._plan(st)      # chunk sizes changed since the forward
+            chunks = self._chunks
             self._ev("field_bwd", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w.offsets.data_ptr(), w.mstart.data_ptr(),

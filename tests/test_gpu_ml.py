@@ -187,3 +187,30 @@ def test_merged_backward_chunking(cuda):
         for a, b in zip(other, res[0]):
             rel = (a - b).norm() / b.norm().clamp_min(1e-30)
             assert rel <= 1e-5, rel
+
+
+@pytest.mark.parametrize("B,K,scale", [(4096, 2, 0.5), (1024, 4, 16.0), (512, 1, 0.5)])
+def test_merged_forward_matches_per_model(cuda, B, K, scale):
+    """rn_field_fwd_merged (chunks of rays, models' tiles interleaved) vs
+    rn_field_fwd: identical per-sample arithmetic, so sigma / rgb and the
+    encoding cache are bit-exact."""
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    outs = []
+    for merged in (True, False):
+        r.merged_fwd = merged
+        ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=esf)
+        w = r.ws
+        off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
+        idx = np.concatenate([np.arange(off[k, rr], off[k, rr] + cnt[k, rr])
+                              for k in range(K) for rr in range(B)]).astype(np.int64)
+        ii = torch.from_numpy(idx).to(cuda)
+        feat = w.feat.view(-1, 64, 2, 8)       # [tile][lane][k-step][8]
+        t, c = ii // 32, ii % 32
+        cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
+        outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
+    r.merged_fwd = False
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
