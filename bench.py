@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--split-bwd", action="store_true",
                     help="backward with one model per block (rn_field_bwd) instead of the "
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
-    ap.add_argument("--max-chunk", type=int, default=4096,
+    ap.add_argument("--max-chunk", type=int, default=1024,
                     help="merged backward: largest chunk of merged samples per queue grab")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
@@ -105,7 +105,7 @@ def main():
     bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
 
     r = FusedMLRenderer(model, gate, B)
-    r.merged_bwd = not args.split_bwd
+    r.merged_bwd = r.merged_bwd and not args.split_bwd
     r.max_chunk = args.max_chunk
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)

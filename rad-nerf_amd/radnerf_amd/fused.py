@@ -115,7 +115,8 @@ class FusedMLRenderer:
         self.feat_cache = True      # field fwd stores the encoding, bwd skips the re-gather
         # backward scatters the K models' grid gradients merged per ray
         # (rn_field_bwd_merged); False: one model per block (rn_field_bwd)
-        self.merged_bwd = True
+        # (K = 1 has nothing to merge: the per-model kernel is 3 % faster there)
+        self.merged_bwd = model.size > 1
         # forward evaluating the K models' tiles of a chunk interleaved
         # (rn_field_fwd_merged, K <= 4): bit-exact with rn_field_fwd and measured
         # no faster (1.31 vs 1.30 ms on C3: the gathers are not L2-miss bound),
@@ -123,7 +124,10 @@ class FusedMLRenderer:
         self.merged_fwd = False
         self.merged_fwd_blocks = 512
         self.merged_blocks = 256
-        self.max_chunk = 4096
+        # chunk of merged samples per queue ticket: 1024 keeps a block's staged
+        # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
+        # 8192 4.50 ms)
+        self.max_chunk = 1024
         self.min_chunk = 512
         self.trace = False          # record HIP events around every launch
         self.events = {}

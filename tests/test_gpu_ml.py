@@ -138,7 +138,7 @@ def _merged_vs_split(cuda, B, K, scale, p=0.5):
         r.merged_bwd = merged
         _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
         out.append(gr)
-    r.merged_bwd = True
+    r.merged_bwd = K > 1
     return r, out
 
 
@@ -178,11 +178,11 @@ def test_merged_backward_chunking(cuda):
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
     r = get_renderer(m, g, B)
     res = []
-    for mc, blocks in ((4096, 256), (64, 37), (300, 3)):
+    for mc, blocks in ((1024, 256), (4096, 256), (64, 37), (300, 3)):
         r.max_chunk, r.merged_blocks = mc, blocks
         _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
         res.append(gr)
-    r.max_chunk, r.merged_blocks = 4096, 256
+    r.max_chunk, r.merged_blocks = 1024, 256
     for other in res[1:]:
         for a, b in zip(other, res[0]):
             rel = (a - b).norm() / b.norm().clamp_min(1e-30)
