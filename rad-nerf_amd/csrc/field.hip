@@ -658,31 +658,34 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
     }
 }
 
-// append this step's finished entries (up to 2 per lane) to the stream rings
+// append this step's finished entries (up to 2 per lane) to the stream rings,
+// lane-major (a lane's even-X and odd-X records adjacent: they share a 64-B
+// segment, so an instruction boundary splits them less often; replay of the
+// bench samples, tools/atomic_sim2.py: 15.18 -> 14.65 requests/sample)
 __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint64_t smask,
                                            uint32_t lvl_off) {
     const uint64_t m0 = __builtin_amdgcn_ballot_w64(e0) & smask;
     const uint64_t m1 = __builtin_amdgcn_ballot_w64(e1) & smask;
-    const uint32_t n0 = (uint32_t)__builtin_popcountll(m0);
     const int s = rn_lane() >> 2;
     uint32_t* base = W.ring + s * 3 * W2_RING;
+    // records of the stream's lower lanes
+    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u)) +
+                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
     if (e0) {
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-        const uint32_t rec = w2_wrap(W.tail + r);
+        const uint32_t rec = w2_wrap(W.tail + below);
         base[rec] = 8u * (lvl_off + W.cur0);
         base[W2_RING + rec] = __float_as_uint(W.a00);
         base[2 * W2_RING + rec] = __float_as_uint(W.a01);
     }
     if (e1) {
-        const uint32_t r = n0 + __builtin_amdgcn_mbcnt_hi(
-                                    (uint32_t)(m1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-        const uint32_t rec = w2_wrap(W.tail + r);
+        const uint32_t rec = w2_wrap(W.tail + below + (e0 ? 1u : 0u));
         base[rec] = 8u * (lvl_off + W.cur1);
         base[W2_RING + rec] = __float_as_uint(W.a10);
         base[2 * W2_RING + rec] = __float_as_uint(W.a11);
     }
-    W.tail = w2_wrap(W.tail + n0 + (uint32_t)__builtin_popcountll(m1));
+    W.tail = w2_wrap(W.tail + (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1)));
 }
 
 __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& sT) {
