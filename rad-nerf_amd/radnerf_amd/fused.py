@@ -116,7 +116,7 @@ class FusedMLRenderer:
         # backward scatters the K models' grid gradients merged per ray
         # (rn_field_bwd_merged); False: one model per block (rn_field_bwd)
         # (K = 1 has nothing to merge: the per-model kernel is 3 % faster there)
-        self.merged_bwd = model.size > 1
+        self.merged_bwd = 1 < model.size <= 8      # rn_field_bwd_merged: K <= 8
         # forward evaluating the K models' tiles of a chunk interleaved
         # (rn_field_fwd_merged, K <= 4): bit-exact with rn_field_fwd and measured
         # no faster (1.31 vs 1.30 ms on C3: the gathers are not L2-miss bound),

@@ -40,6 +40,8 @@ __global__ void __launch_bounds__(256) k_probe(float* buf, uint32_t nseg, int it
     if (VAR == 4 || VAR == 5) {
         base = buf + (size_t)xcc_id() * nseg * 16;
     }
+    uint32_t acc = 0;
+    float accf = 0.f;
     for (int i = 0; i < iters; ++i) {
         const uint32_t seg = hash32(wave * 1315423911u + i * 64 + sidx) % nseg;
         const size_t off = (size_t)seg * 16 + within;
@@ -61,12 +63,21 @@ __global__ void __launch_bounds__(256) k_probe(float* buf, uint32_t nseg, int it
         } else if (VAR == 9) {
             double* p = (double*)base + (size_t)seg * 8 + (within & 7);
             __hip_atomic_fetch_add(p, 1.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 10) {
+            // returning u32 add: keep the result live (sum into a register)
+            acc += __hip_atomic_fetch_add((uint32_t*)(base + off), 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        } else if (VAR == 11) {
+            accf += __hip_atomic_fetch_add(base + off, 1.0f, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
         } else if (VAR == 7) {
             typedef _Float16 h2 __attribute__((ext_vector_type(2)));
             h2 hv = {(_Float16)1.0f, (_Float16)1.0f};
             __builtin_amdgcn_global_atomic_fadd_v2f16((h2*)(base + off), hv);
         }
     }
+    if (VAR == 10 && acc == 0xdeadbeefu) buf[0] = 1.f;
+    if (VAR == 11 && accf == -1.f) buf[0] = 1.f;
 }
 
 template <int VAR>
@@ -114,6 +125,12 @@ int main() {
     for (int segs : {8, 16}) {
         if (run<8>(buf, nseg, iters, segs, "u64_agent_8B_lanes")) return 1;
         if (run<9>(buf, nseg, iters, segs, "f64_agent_8B_lanes")) return 1;
+        if (run<2>(buf, nseg, iters, segs, "u32_agent")) return 1;
+    }
+    for (int segs : {4, 16}) {
+        if (run<10>(buf, nseg, iters, segs, "u32_agent_return")) return 1;
+        if (run<11>(buf, nseg, iters, segs, "f32_agent_return")) return 1;
+        if (run<0>(buf, nseg, iters, segs, "f32_agent")) return 1;
         if (run<2>(buf, nseg, iters, segs, "u32_agent")) return 1;
     }
     // small L2-resident footprint (256 KB per XCD copy)
