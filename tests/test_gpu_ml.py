@@ -214,3 +214,17 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
     r.merged_fwd = False
     for a, b in zip(*outs):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("p,K", [(0.0, 2), (1.0, 3)])
+def test_merged_backward_edge_occupancy(cuda, p, K):
+    """Empty grid (no samples at all: zero chunks) and a full grid with K = 3
+    (odd model count, many 1024-capped rays): merged = per-model backward."""
+    B = 256
+    r, (gm, gs) = _merged_vs_split(cuda, B, K, 0.5, p=p)
+    for a, b in zip(gm, gs):
+        rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+        assert rel <= 1e-5, rel
+    if p == 0.0:
+        assert int(r.ws.meta[1]) == 0
+        assert float(gm[0].abs().max()) == 0.0
