@@ -230,7 +230,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const uint32_t* level_res, const float* level_scale,
                         const float* xyz_min, const float* extent, const void* frags,
                         float* sigma, float* rgb, void* feat_cache, int32_t blocks,
-                        void* stream);
+                        int32_t threads, void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------
  * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)

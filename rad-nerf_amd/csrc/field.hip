@@ -1285,7 +1285,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
 #define FM_KMAX 4
 
 template <int CACHE>
-__global__ void __launch_bounds__(512)
+__global__ void __launch_bounds__(1024)
 k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
     __shared__ LvTab sT;
@@ -1627,9 +1627,10 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const uint32_t* level_res, const float* level_scale,
                         const float* xyz_min, const float* extent, const void* frags,
                         float* sigma, float* rgb, void* feat_cache, int32_t blocks,
-                        void* stream) {
+                        int32_t threads, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && blocks >= 1,
                  "bad sizes (n_models <= 4)");
+    RN_CHECK_ARG(threads >= 64 && threads <= 1024 && threads % 64 == 0, "threads: 64..1024, waves");
     RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets &&
                  chunk_first && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && sigma && rgb, "null pointer");
@@ -1649,8 +1650,8 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         rn_set_error("%s: ticket reset failed", __func__);
         return 2;
     }
-    if (feat_cache) k_field_fwd_merged<CACHE_WRITE><<<blocks, 512, lds, st>>>(a, m);
-    else k_field_fwd_merged<CACHE_NONE><<<blocks, 512, lds, st>>>(a, m);
+    if (feat_cache) k_field_fwd_merged<CACHE_WRITE><<<blocks, threads, lds, st>>>(a, m);
+    else k_field_fwd_merged<CACHE_NONE><<<blocks, threads, lds, st>>>(a, m);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -48,7 +48,7 @@ SIGNATURES = {
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
                             P, P, P, P, P, P, P, P, I64, P, I32, I32, P],
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,
-                            I32, P],
+                            I32, I32, P],
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],

@@ -118,11 +118,13 @@ class FusedMLRenderer:
         # (K = 1 has nothing to merge: the per-model kernel is 3 % faster there)
         self.merged_bwd = 1 < model.size <= 8      # rn_field_bwd_merged: K <= 8
         # forward evaluating the K models' tiles of a chunk interleaved
-        # (rn_field_fwd_merged, K <= 4): bit-exact with rn_field_fwd and measured
-        # no faster (1.31 vs 1.30 ms on C3: the gathers are not L2-miss bound),
-        # so off by default
-        self.merged_fwd = False
-        self.merged_fwd_blocks = 512
+        # (rn_field_fwd_merged, K <= 4; bit-exact with rn_field_fwd).  One
+        # 8-wave block per CU keeps a chunk's rays in that CU's L1, so the second
+        # model's corners hit lines the first fetched: C3 1.12 ms vs 1.30 ms
+        # (tools/fwd_blocks_sweep.py; 2 blocks per CU 1.17, 3 x 4 waves 1.35)
+        self.merged_fwd = model.size <= 4
+        self.merged_fwd_blocks = 256
+        self.merged_fwd_threads = 512
         self.merged_blocks = 256
         # chunk of merged samples per queue ticket: 1024 keeps a block's staged
         # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
@@ -237,7 +239,7 @@ class FusedMLRenderer:
                      w.seg_count.data_ptr(), w.offsets.data_ptr(), self._chunks.data_ptr(),
                      w.queue.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
                      w.rgb.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
-                     self.merged_fwd_blocks, st)
+                     self.merged_fwd_blocks, self.merged_fwd_threads, st)
         elif fwd:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),
                      w.feat.data_ptr() if self.feat_cache else None, self.fwd_blocks, st)
