@@ -1348,16 +1348,28 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
 // Merged order of the K models' samples per ray (ray-major, then t, ties by
 // model): perm[mstart[r] + rank] = sample.  One wave per ray; each sample's
 // rank = its index in its (model, ray) run + the samples of the other models
-// of the ray that precede it (binary search; t increases along a run).
-__global__ void __launch_bounds__(256)
+// of the ray that precede it (binary search; t increases along a run).  The
+// ray's K runs are staged in the wave's LDS slice when they fit (always for
+// K = 2), so the searches are LDS reads instead of dependent global loads.
+#define PLAN_WAVES 4
+#define PLAN_LDS 2048      // floats per wave
+
+__global__ void __launch_bounds__(PLAN_WAVES * 64)
 k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
            const int32_t* __restrict__ seg_base, const int32_t* __restrict__ seg_count,
            const float* __restrict__ ts, int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
-    const int r = blockIdx.x * (blockDim.x / RN_WAVE) + threadIdx.x / RN_WAVE;
-    if (r >= B) return;
+    __shared__ float sT[PLAN_WAVES][PLAN_LDS];
+    const int wid = threadIdx.x / RN_WAVE;
+    const int r = blockIdx.x * PLAN_WAVES + wid;
+    if (r >= B) return;                      // wave-uniform; no block barrier below
     const int lane = rn_lane();
-    int ms = 0;
-    for (int k = 0; k < K; ++k) ms += offsets[k * B + r] - seg_base[k];
+    int ms = 0, tot_r = 0;
+    int cnt[MB_KMAX], off[MB_KMAX], loc[MB_KMAX];
+    for (int k = 0; k < K; ++k) {
+        cnt[k] = counts[k * B + r]; off[k] = offsets[k * B + r];
+        ms += off[k] - seg_base[k];
+        loc[k] = tot_r; tot_r += cnt[k];
+    }
     if (lane == 0) {
         mstart[r] = ms;
         if (r == 0) {
@@ -1366,23 +1378,29 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
             mstart[B] = tot;
         }
     }
+    const bool staged = tot_r <= PLAN_LDS;
+    float* st = sT[wid];
+    if (staged) {
+        for (int k = 0; k < K; ++k)
+            for (int i = lane; i < cnt[k]; i += RN_WAVE) st[loc[k] + i] = ts[off[k] + i];
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    }
     for (int k = 0; k < K; ++k) {
-        const int n = counts[k * B + r], o = offsets[k * B + r];
-        for (int i = lane; i < n; i += RN_WAVE) {
-            const float t = ts[o + i];
+        for (int i = lane; i < cnt[k]; i += RN_WAVE) {
+            const float t = staged ? st[loc[k] + i] : ts[off[k] + i];
             int pos = i;
             for (int k2 = 0; k2 < K; ++k2) {
                 if (k2 == k) continue;
-                const int n2 = counts[k2 * B + r], o2 = offsets[k2 * B + r];
-                int lo = 0, hi = n2;             // count of t2 < t (k2 > k) or t2 <= t (k2 < k)
+                int lo = 0, hi = cnt[k2];        // count of t2 < t (k2 > k) or t2 <= t (k2 < k)
                 while (lo < hi) {
                     const int mid = (lo + hi) >> 1;
-                    const float t2 = ts[o2 + mid];
+                    const float t2 = staged ? st[loc[k2] + mid] : ts[off[k2] + mid];
                     if (t2 < t || (k2 < k && t2 == t)) lo = mid + 1; else hi = mid;
                 }
                 pos += lo;
             }
-            perm[ms + pos] = o + i;
+            perm[ms + pos] = off[k] + i;
         }
     }
 }
@@ -1560,7 +1578,7 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
     RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1, "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
                  chunk_first && queue, "null pointer");
-    k_bwd_plan<<<nblk(n_rays, 4), 256, 0, (hipStream_t)stream>>>(
+    k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(

@@ -61,7 +61,7 @@ def streams(ray, max_chunk, min_chunk=512, parts=8):
     return chunk * parts + part
 
 
-def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0):
+def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0, ent_per_seg=8):
     n = len(u)
     total = 0
     last = np.r_[sid[1:] != sid[:-1], True]                      # last sample of a stream
@@ -80,7 +80,7 @@ def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0
                     idx = (X + Y * res + Z * res * res) % hs
                 else:
                     idx = (X ^ ((Y * 2654435761) & 0xFFFFFFFF) ^ ((Z * 805459861) & 0xFFFFFFFF)) % hs
-                seg = (idx + off) // 8
+                seg = (idx + off) // ent_per_seg
                 ent = (X * 4096 + Y) * 4096 + Z
                 # entry at position i leaves at i+1 if the next entry differs (same stream),
                 # or at the stream end (flush after the last step)
@@ -131,11 +131,12 @@ def main():
     parts = int(sys.argv[4]) if len(sys.argv) > 4 else 8
     lane_major = len(sys.argv) > 5 and sys.argv[5] == "lane"
     cut_min = int(sys.argv[6]) if len(sys.argv) > 6 else 0
+    eps = int(sys.argv[7]) if len(sys.argv) > 7 else 8
     u, ray, lv = merged_samples(B)
     sid = streams(ray, mc, parts=parts)
     print(f"B {B} samples {len(u)} max_chunk {mc} issue {issue} parts {parts} "
           f"{'lane' if lane_major else 'slot'}-major: "
-          f"requests/sample {requests(u, lv, sid, issue, lane_major=lane_major, cut_min=cut_min):.2f} (cut_min {cut_min})")
+          f"requests/sample {requests(u, lv, sid, issue, lane_major=lane_major, cut_min=cut_min, ent_per_seg=eps):.2f} (cut_min {cut_min}, entries/segment {eps})")
 
 
 if __name__ == "__main__":
