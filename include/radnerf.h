@@ -214,7 +214,23 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const void* frags, const float* dL_dsigma, const float* dL_drgb,
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
+                        int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
                         void* stream);
+
+/* Exact integer accumulation of the merged backward's grid gradient
+ * (optional; igrad_lo == NULL keeps fp32 atomics into grid_grad).  With
+ * igrad_lo / igrad_carry (int32, one per grid_grad element, zero on entry) and
+ * igrad_scale (device f32, from rn_seed_scale), rn_field_bwd_merged adds each
+ * contribution as rint(v * scale) with returning u32 atomics plus exact
+ * carries; rn_igrad_to_f32 then adds (carry * 2^32 + lo) / scale into
+ * grid_grad and re-zeroes the integer arrays.  Order-independent, so the grid
+ * gradient is bitwise reproducible.  rn_seed_scale: scale = 2^(26 - e) for the
+ * step's largest seed M in [2^(e-1), 2^e) (work: 1 u32 scratch word).      */
+int rn_seed_scale(const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
+                  const float* sigma, const float* dL_dsigma, const float* dL_drgb,
+                  uint32_t* work, float* scale, void* stream);
+int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const float* scale,
+                    float* grid_grad, void* stream);
 
 /* Merged forward (fused training path, n_models <= 4): same outputs as
  * rn_field_fwd in compact mode, but blocks take rn_bwd_plan's chunks (queue

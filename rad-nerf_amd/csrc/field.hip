@@ -611,38 +611,94 @@ struct Walk2 {
     uint32_t head, tail;   // per lane: its stream's ring head / tail, in [0, W2_RING)
     uint32_t ex0, ex1, ey, ez, cur0, cur1;   // even-X / odd-X entries of the row
     float a00, a01, a10, a11;                // their accumulated feature gradients
+    // integer mode: the two newest issues, checked for carries one issue late
+    int32_t oldA, loA, hiA, oldB, loB, hiB;
+    uint32_t offA, offB;
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     W.ring = ring; W.head = 0; W.tail = 0;
     W.ex0 = W2_NONE; W.ex1 = W2_NONE; W.ey = 0; W.ez = 0; W.cur0 = 0; W.cur1 = 0;
     W.a00 = W.a01 = W.a10 = W.a11 = 0.f;
+    W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
+    W.offA = W.offB = 0;
+}
+
+// Exact integer accumulation of the grid gradient (IG mode).  Each record
+// value v becomes q = rint(v * 2^scale_exp) (int64), added as a 32-bit low
+// word with a returning atomic; the high word plus any signed overflow of the
+// low word (read from the returned old value) goes to a parallel carry array,
+// so every entry holds carry * 2^32 + low exactly: sums are order-independent
+// (bitwise reproducible) and u32 atomics run 28 % faster than f32 at the
+// memory side (profiles/r01/atomic_probe.json).  A carry add is rare.
+struct IntGrad {
+    __amdgpu_buffer_rsrc_t lo, carry;   // int32 [entries][2] each (built in the kernel)
+    float scale;                        // 2^scale_exp (loaded from scale_ptr)
+    int32_t* lo_ptr; int32_t* carry_ptr; const float* scale_ptr;
+    uint32_t bytes;
+};
+
+__device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, uint32_t off,
+                                         const IntGrad& G) {
+    const int32_t nw = (int32_t)((uint32_t)old + (uint32_t)lo);
+    const bool ov = ((old ^ nw) & (lo ^ nw)) < 0;
+    const int32_t c = hi + (ov ? (lo > 0 ? 1 : -1) : 0);
+    if (c != 0) __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(c, G.carry, (int)off, 0, 0);
 }
 
 __device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? v - W2_RING : v; }
 
 // issue up to 32 records of stream s (wave-uniform) as one atomic instruction
+template <bool IG>
 __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
-                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+                                            __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
+                                            int dbg) {
     const int lane = rn_lane();
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
     asm volatile("" ::: "memory");
+    if (IG) {
+        // the issue two back has had a whole issue's time to return
+        ig_check(W.oldA, W.loA, W.hiA, W.offA, G);
+        W.oldA = W.oldB; W.loA = W.loB; W.hiA = W.hiB; W.offA = W.offB;
+        W.oldB = 0; W.loB = 0; W.hiB = 0;
+    }
     if ((uint32_t)lane < 2u * cnt) {
         const uint32_t rec = w2_wrap(h + (lane >> 1));
         const uint32_t* base = W.ring + s * 3 * W2_RING;
         const uint32_t off = base[rec] + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
-        if (dbg & 1) asm volatile("" :: "v"(off), "v"(v));
-        else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
-                                                             (int)off, 0, 0);
+        if (dbg & 1) {
+            asm volatile("" :: "v"(off), "v"(v));
+        } else if (IG) {
+            // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
+            const float x = rintf(__uint_as_float(v) * G.scale);
+            const long long q = (long long)x;
+            const int32_t lo = (int32_t)(uint32_t)(unsigned long long)q;
+            W.loB = lo;
+            W.hiB = (int32_t)((q - (long long)lo) >> 32);
+            W.offB = off;
+            W.oldB = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(lo, G.lo, (int)off, 0, 0);
+        } else {
+            __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
+                                                            (int)off, 0, 0);
+        }
     }
     asm volatile("" ::: "memory");
     if ((lane >> 2) == s) W.head = w2_wrap(W.head + cnt);
 }
 
+// integer mode: settle the two outstanding issues (end of a chunk)
+__device__ __forceinline__ void walk2_settle(Walk2& W, const IntGrad& G) {
+    ig_check(W.oldA, W.loA, W.hiA, W.offA, G);
+    ig_check(W.oldB, W.loB, W.hiB, W.offB, G);
+    W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
+}
+
 // issue every stream with >= min_cnt pending (min_cnt 0: drain all)
+template <bool IG>
 __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
-                                            __amdgpu_buffer_rsrc_t grad_rs, int dbg) {
+                                            __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
+                                            int dbg) {
     const bool lead = (rn_lane() & 3) == 0;
     for (;;) {
         const uint32_t pend = W.tail >= W.head ? W.tail - W.head : W.tail + W2_RING - W.head;
@@ -651,7 +707,7 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
         while (m) {
             const int s = __builtin_ctzll(m) >> 2;
             const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
-            walk2_issue(W, s, p < 32u ? p : 32u, grad_rs, dbg);
+            walk2_issue<IG>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
             m &= m - 1;
         }
         if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
@@ -696,9 +752,11 @@ __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& 
 
 // walk one window: eighth e's samples are rows [32e, 32e + ne) of sG/sU
 // (ne per lane: its eighth's count; n0 = the largest, wave-uniform)
+template <bool IG>
 __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT,
                                              const float* sG_, const float* sU_, int ne, int n0,
-                                             __amdgpu_buffer_rsrc_t grad_rs, Walk2& W, int dbg) {
+                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
+                                             Walk2& W, int dbg) {
     lds_cf* sG = (lds_cf*)sG_;
     lds_cf* sU = (lds_cf*)sU_;
     const int lane = rn_lane();
@@ -748,17 +806,20 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
             W.cur1 = lc.dense ? (d1 >= lc.hs ? d1 - lc.hs : d1) : ((X1 ^ hb) & (lc.hs - 1u));
             W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
         }
-        walk2_drain(W, 32u, grad_rs, dbg);
+        walk2_drain<IG>(W, 32u, grad_rs, G, dbg);
     }
 }
 
 // end of a chunk: emit every live entry and drain the rings completely
+template <bool IG>
 __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
-                                          __amdgpu_buffer_rsrc_t grad_rs, Walk2& W, int dbg) {
+                                          __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
+                                          Walk2& W, int dbg) {
     const LvConst lc = walk2_level(a, sT);
     const uint64_t smask = 0xfull << (4 * (rn_lane() >> 2));
     walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, smask, lc.off);
-    walk2_drain(W, 0u, grad_rs, dbg);
+    walk2_drain<IG>(W, 0u, grad_rs, G, dbg);
+    if (IG) walk2_settle(W, G);
     walk2_begin(W, W.ring);
 }
 
@@ -1091,9 +1152,14 @@ __device__ __forceinline__ void dw_unpark(const float* p, f32x16& A, f32x16& B) 
     }
 }
 
-template <int CACHE, bool ABL>
+template <int CACHE, bool ABL, bool IG>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
-k_field_bwd_merged(FieldArgs a, MergeArgs m) {
+k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
+    if (IG) {
+        G.scale = *G.scale_ptr;
+        G.lo = rn_rsrc(G.lo_ptr, G.bytes);
+        G.carry = rn_rsrc(G.carry_ptr, G.bytes);
+    }
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[BWD_WAVES];
@@ -1254,11 +1320,11 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m) {
             if (__syncthreads_or(nz) && !(dbg & 32)) {
                 const int ne = max(0, min(32, elen_lane - w0));
                 const int n0 = max(0, min(32, min(E, n_p) - w0));
-                walk2_window(a, sT, sG, sU, ne, n0, grad_rs, W, dbg);
+                walk2_window<IG>(a, sT, sG, sU, ne, n0, grad_rs, G, W, dbg);
             }
             __syncthreads();
         }
-        walk2_end(a, sT, grad_rs, W, dbg);
+        walk2_end<IG>(a, sT, grad_rs, G, W, dbg);
         __syncthreads();                         // rings (image region) drained
     }
     // ---- flush every model's dW (the current one from registers)
@@ -1343,6 +1409,50 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
             }
         }
     }
+}
+
+
+// Integer-mode scale: 2^(26 - e) with 2^(e-1) <= M < 2^e, M the largest
+// backward seed of the step (|dL/dsigma * sigma|, |dL/drgb|), so a seed-sized
+// contribution is ~2^26 units; larger ones carry exactly.
+__global__ void __launch_bounds__(256)
+k_seed_max(const int32_t* __restrict__ seg_base, const int32_t* __restrict__ seg_count,
+           const float* __restrict__ sigma, const float* __restrict__ dsigma,
+           const float* __restrict__ drgb, uint32_t* __restrict__ mbits) {
+    const int k = blockIdx.y;
+    const int64_t base = seg_base[k], n = seg_count[k];
+    float mx = 0.f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s = base + i;
+        mx = fmaxf(mx, fabsf(dsigma[s] * sigma[s]));
+        mx = fmaxf(mx, fmaxf(fabsf(drgb[3 * s]), fmaxf(fabsf(drgb[3 * s + 1]), fabsf(drgb[3 * s + 2]))));
+    }
+    mx = rn_wave_max(mx);
+    if (rn_lane() == 0 && mx > 0.f && isfinite(mx)) atomicMax(mbits, __float_as_uint(mx));
+}
+
+__global__ void k_seed_scale(const uint32_t* __restrict__ mbits, float* __restrict__ scale) {
+    const float m = __uint_as_float(*mbits);
+    float sc = 1.0f;
+    if (m > 0.f) {
+        int e;
+        frexpf(m, &e);                   // m = f * 2^e, f in [0.5, 1)
+        sc = scalbnf(1.0f, max(-100, min(100, 26 - e)));
+    }
+    *scale = sc;
+}
+
+// grid_grad += (carry * 2^32 + lo) / scale; lo = carry = 0 for the next step
+__global__ void __launch_bounds__(256)
+k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
+               const float* __restrict__ scale, float* __restrict__ grad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = ((double)carry[i] * 4294967296.0 + (double)lo[i]) / (double)*scale;
+    grad[i] += (float)v;
+    lo[i] = 0;
+    carry[i] = 0;
 }
 
 // Merged order of the K models' samples per ray (ray-major, then t, ties by
@@ -1598,7 +1708,9 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const void* frags, const float* dL_dsigma, const float* dL_drgb,
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
+                        int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
                         void* stream) {
+    RN_CHECK_ARG(!igrad_lo || (igrad_carry && igrad_scale), "integer mode needs carry and scale");
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX && blocks >= 1 &&
                  max_samples >= 1 && max_chunk >= 1, "bad sizes");
     RN_CHECK_ARG(scratch_rows >= (int64_t)max_chunk + (int64_t)n_models * max_samples,
@@ -1626,12 +1738,21 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         rn_set_error("%s: ticket reset failed", __func__);
         return 2;
     }
-    if (a.dbg) {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
-        else k_field_bwd_merged<CACHE_NONE, true><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+    IntGrad G{};
+    if (igrad_lo) {
+        G.bytes = 2 * a.grid_bytes;            // int32 arrays, same size as the f32 grad
+        G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
+    }
+    const dim3 blk(BWD_WAVES * 64);
+    if (igrad_lo) {
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, true><<<blocks, blk, 0, st>>>(a, m, G);
+        else k_field_bwd_merged<CACHE_NONE, false, true><<<blocks, blk, 0, st>>>(a, m, G);
+    } else if (a.dbg) {
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, true, false><<<blocks, blk, 0, st>>>(a, m, G);
+        else k_field_bwd_merged<CACHE_NONE, true, false><<<blocks, blk, 0, st>>>(a, m, G);
     } else {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
-        else k_field_bwd_merged<CACHE_NONE, false><<<blocks, BWD_WAVES * 64, 0, st>>>(a, m);
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, false><<<blocks, blk, 0, st>>>(a, m, G);
+        else k_field_bwd_merged<CACHE_NONE, false, false><<<blocks, blk, 0, st>>>(a, m, G);
     }
     RN_CHECK_LAUNCH();
     return 0;
@@ -1670,6 +1791,36 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     }
     if (feat_cache) k_field_fwd_merged<CACHE_WRITE><<<blocks, threads, lds, st>>>(a, m);
     else k_field_fwd_merged<CACHE_NONE><<<blocks, threads, lds, st>>>(a, m);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_seed_scale(const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
+                  const float* sigma, const float* dL_dsigma, const float* dL_drgb,
+                  uint32_t* work, float* scale, void* stream) {
+    RN_CHECK_ARG(n_models >= 1, "bad sizes");
+    RN_CHECK_ARG(seg_base && seg_count && sigma && dL_dsigma && dL_drgb && work && scale,
+                 "null pointer");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(work, 0, sizeof(uint32_t), st) != hipSuccess) {
+        rn_set_error("%s: memset failed", __func__);
+        return 2;
+    }
+    k_seed_max<<<dim3(256, n_models), 256, 0, st>>>(seg_base, seg_count, sigma, dL_dsigma,
+                                                     dL_drgb, work);
+    RN_CHECK_LAUNCH();
+    k_seed_scale<<<1, 1, 0, st>>>(work, scale);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const float* scale,
+                    float* grid_grad, void* stream) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    if (n == 0) return 0;
+    RN_CHECK_ARG(igrad_lo && igrad_carry && scale && grid_grad, "null pointer");
+    k_igrad_to_f32<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, igrad_lo, igrad_carry, scale,
+                                                                   grid_grad);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -95,6 +95,12 @@ __host__ __device__ __forceinline__ uint32_t rn_morton3d_invert(uint32_t x) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int rn_lane() { return threadIdx.x & (RN_WAVE - 1); }
 
+__device__ __forceinline__ float rn_wave_max(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off));
+    return v;
+}
+
 __device__ __forceinline__ float rn_wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);

@@ -130,6 +130,12 @@ class FusedMLRenderer:
         # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
         # 8192 4.50 ms)
         self.max_chunk = 1024
+        # exact integer accumulation of the grid gradient (rn_seed_scale +
+        # returning u32 atomics with carries + rn_igrad_to_f32): bitwise
+        # reproducible grid gradients, but each issue waits for the previous
+        # one's return (the compiler's vmcnt(0)): 4.33 vs 3.81 ms on C3, so the
+        # default stays fp32 atomics
+        self.int_grad = False
         self.min_chunk = 512
         self.trace = False          # record HIP events around every launch
         self.events = {}
@@ -249,6 +255,19 @@ class FusedMLRenderer:
                                                     min(self.min_chunk, self.max_chunk)):
                 self._plan(st)      # chunk sizes changed since the forward
             chunks = self._chunks
+            ig = (None, None, None)
+            if self.int_grad:
+                n_g = grid_grad.numel()
+                if getattr(w, "_igrad", None) is None or w._igrad[0].numel() != n_g:
+                    z = dict(device=grid_grad.device, dtype=torch.int32)
+                    w._igrad = (torch.zeros(n_g, **z), torch.zeros(n_g, **z),
+                                torch.ones(1, device=grid_grad.device),
+                                torch.zeros(1, **z))
+                lo, carry, scale, work = w._igrad
+                self._ev("seed_scale", L.seed_scale, w.seg_base.data_ptr(),
+                         w.seg_count.data_ptr(), m.size, w.sigma.data_ptr(), w.dsigma.data_ptr(),
+                         w.drgb.data_ptr(), work.data_ptr(), scale.data_ptr(), st)
+                ig = (lo.data_ptr(), carry.data_ptr(), scale.data_ptr())
             self._ev("field_bwd", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w.offsets.data_ptr(), w.mstart.data_ptr(),
@@ -257,7 +276,10 @@ class FusedMLRenderer:
                      *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
                      dw.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
                      scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
-                     self.merged_blocks, st)
+                     self.merged_blocks, *ig, st)
+            if self.int_grad:
+                self._ev("igrad_to_f32", L.igrad_to_f32, grid_grad.numel(), ig[0], ig[1], ig[2],
+                         grid_grad.data_ptr(), st)
         else:
             self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
                      w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),

@@ -1,0 +1,75 @@
+"""Kernel ablation on the bench workload (dev tool): times field_bwd with parts
+switched off (rn_set_debug_flags) interleaved in one process (rule 24 of
+cdna_hip_programming.md §5.4).  bit0: no grid atomics, bit1: no dW, bit2: no
+grid scatter at all."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rad-nerf_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from radnerf_amd import synthetic as S  # noqa: E402
+from radnerf_amd._lib import lib  # noqa: E402
+from radnerf_amd.fused import FusedMLRenderer  # noqa: E402
+from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
+
+
+def main():
+    flags = sys.argv[1:] or ["0", "i0", "s0"]
+    dev = torch.device("cuda")
+    B, K = 8192, 2
+    m = MNGP(0.5, size=K, seed=3).to(dev)
+    g = Ray_Gate(K, seed=4).to(dev)
+    bits = S.bitfields(K, 1, p=0.5)
+    with torch.no_grad():
+        for i in range(K):
+            getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B))
+    nz = torch.from_numpy(S.noise(K, B)).to(dev)
+    sd = [torch.from_numpy(a).to(dev) for a in S.loss_seeds(B, K)]
+    bg = torch.ones(3, device=dev)
+    r = FusedMLRenderer(m, g, B)
+    _, _, _, gt, _ = r.forward(o, d, d, nz, bg)
+    gg = torch.zeros_like(m.xyz_encoder.params)
+    mg = torch.zeros_like(m.mlp_params)
+    ag = torch.zeros_like(g.params)
+    r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
+    L = lib()
+    st = torch.cuda.current_stream().cuda_stream
+    # tokens: "<flags>" = field_bwd (merged) with debug flags, "s<flags>" = the
+    # per-model field_bwd, "f<flags>" = field_fwd
+    times = {f: [] for f in flags}
+    fwd = []
+    for rnd in range(5):
+        for f in flags:
+            L.set_debug_flags(int(f.lstrip("fsi")))
+            r.merged_bwd = not f.startswith("s"); r.int_grad = f.startswith("i")
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            if f.startswith("f"):
+                r._field(True, o, d, st)
+            else:
+                r._field(False, o, d, st, gg, mg)
+            b.record()
+            torch.cuda.synchronize()
+            times[f].append(a.elapsed_time(b))
+        L.set_debug_flags(0)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        r._field(True, o, d, st)
+        b.record()
+        torch.cuda.synchronize()
+        fwd.append(a.elapsed_time(b))
+    out = {"samples": r.ws.n_samples(), "field_fwd_ms": float(np.median(fwd)),
+           "field_bwd_ms": {str(f): float(np.median(v)) for f, v in times.items()
+                            if not f.startswith("f")},
+           "field_fwd_flags_ms": {str(f): float(np.median(v)) for f, v in times.items()
+                                  if f.startswith("f")}}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
