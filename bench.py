@@ -68,6 +68,8 @@ def parse():
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
     ap.add_argument("--max-chunk", type=int, default=1024,
                     help="merged backward: largest chunk of merged samples per queue grab")
+    ap.add_argument("--head-chunk", type=int, default=0,
+                    help="merged passes: first chunk per block (0 = none)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
                          "multi-rank path on one GPU")
@@ -107,6 +109,7 @@ def main():
     r = FusedMLRenderer(model, gate, B)
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     r.max_chunk = args.max_chunk
+    r.head_chunk = args.head_chunk
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
 

@@ -188,10 +188,11 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * scattered in merged per-ray (ray, t) order, so samples of different models
  * on one ray share atomic requests.
  * rn_bwd_plan builds the merged order (mstart [n_rays + 1] i32, perm [total]
- * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: chunks of
- * max_chunk merged samples for the first 7/8 of the work, then min_chunk;
+ * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: head_chunks
+ * chunks of head_size merged samples (one per block, so the first scatter
+ * starts early), then max_chunk up to 7/8 of the work, then min_chunk;
  * queue [3] i32 = bwd ticket, chunk count, fwd ticket).  cap_chunks must bound the chunk
- * count: >= total/max_chunk + total/(8*min_chunk) + 2.
+ * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2.
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
  * stages 144-B rows in its scratch slice (scratch: blocks x scratch_rows x 36
  * f32, scratch_rows >= max_chunk + n_models * max_samples) and parks per-model
@@ -201,8 +202,9 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * the shared xyz_encoder's).                                               */
 int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
-                int32_t max_chunk, int32_t min_chunk, int32_t cap_chunks, int32_t* mstart,
-                int32_t* perm, int32_t* chunk_first, int32_t* queue, void* stream);
+                int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
+                int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
+                int32_t* queue, void* stream);
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* offsets, const int32_t* mstart, const int32_t* perm,

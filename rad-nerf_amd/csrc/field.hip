@@ -1520,24 +1520,44 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
 // min_chunk (a short tail: blocks finish together).  Chunk c holds the rays
 // whose merged start lies in [bound(c), bound(c+1)), so it is whole rays of
 // at most max_chunk + K * max_samples samples (possibly none).
-__device__ __forceinline__ void chunk_plan(int total, int max_chunk, int min_chunk, int& c1,
-                                           int& n_chunks) {
-    c1 = (total - total / 8) / max_chunk;
-    const int rest = total - c1 * max_chunk;
-    n_chunks = c1 + (rest + min_chunk - 1) / min_chunk;
+struct ChunkPlan {
+    int head_n, head, max_chunk, min_chunk, c1, n;
+    __device__ int bound(int c) const {
+        const int H = head_n * head;
+        if (c < head_n) return c * head;
+        if (c <= c1) return H + (c - head_n) * max_chunk;
+        return H + (c1 - head_n) * max_chunk + (c - c1) * min_chunk;
+    }
+};
+
+// head_n chunks of `head` samples first (one per block: the scatter, and so the
+// atomics, start after a short MLP phase instead of a full chunk's), then
+// max_chunk up to 7/8 of the work, then min_chunk
+__device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head, int max_chunk,
+                                                int min_chunk) {
+    ChunkPlan p;
+    p.head = head; p.max_chunk = max_chunk; p.min_chunk = min_chunk;
+    const int main_end = total - total / 8;
+    p.head_n = head > 0 ? min(head_n, main_end / head) : 0;
+    const int H = p.head_n * head;
+    p.c1 = p.head_n + (main_end > H ? (main_end - H) / max_chunk : 0);
+    const int rest = total - p.bound(p.c1);
+    p.n = p.c1 + (rest > 0 ? (rest + min_chunk - 1) / min_chunk : 0);
+    return p;
 }
 
 __global__ void __launch_bounds__(256)
-k_bwd_chunks(int B, const int32_t* __restrict__ mstart, int max_chunk, int min_chunk,
-             int cap_chunks, int32_t* __restrict__ chunk_first, int32_t* __restrict__ queue) {
+k_bwd_chunks(int B, const int32_t* __restrict__ mstart, int head_n, int head, int max_chunk,
+             int min_chunk, int cap_chunks, int32_t* __restrict__ chunk_first,
+             int32_t* __restrict__ queue) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = mstart[B];
-    int c1, n;
-    chunk_plan(total, max_chunk, min_chunk, c1, n);
+    const ChunkPlan p = chunk_plan(total, head_n, head, max_chunk, min_chunk);
+    const int n = p.n;
     if (c == 0) { queue[0] = 0; queue[1] = n < cap_chunks ? n : cap_chunks; queue[2] = 0; }
     if (c > n || c > cap_chunks) return;
     if (c == n || c == cap_chunks) { chunk_first[c] = B; return; }
-    const int bound = c <= c1 ? c * max_chunk : c1 * max_chunk + (c - c1) * min_chunk;
+    const int bound = p.bound(c);
     int lo = 0, hi = B;                       // first ray with mstart >= bound
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -1682,17 +1702,20 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
 
 int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
-                int32_t max_chunk, int32_t min_chunk, int32_t cap_chunks, int32_t* mstart,
-                int32_t* perm, int32_t* chunk_first, int32_t* queue, void* stream) {
+                int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
+                int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
+                int32_t* queue, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX, "bad sizes");
-    RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1, "bad chunk sizes");
+    RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1 && head_chunks >= 0 &&
+                 head_size >= 0 && head_size <= max_chunk, "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
                  chunk_first && queue, "null pointer");
     k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
-        (int)n_rays, mstart, max_chunk, min_chunk, cap_chunks, chunk_first, queue);
+        (int)n_rays, mstart, head_chunks, head_size, max_chunk, min_chunk, cap_chunks, chunk_first,
+        queue);
     RN_CHECK_LAUNCH();
     return 0;
 }

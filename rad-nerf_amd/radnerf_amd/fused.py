@@ -65,9 +65,9 @@ class Workspace:
         self._bwd_scratch = None
         self._chunks = None
 
-    def chunk_list(self, max_chunk, min_chunk):
+    def chunk_list(self, max_chunk, min_chunk, head_chunks=0):
         """rn_bwd_plan's chunk list, sized for the workspace capacity."""
-        cap = self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2
+        cap = head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2
         if self._chunks is None or self._chunks.numel() < cap + 1:
             self._chunks = torch.empty(cap + 1, device=self.device, dtype=torch.int32)
         return cap, self._chunks
@@ -137,6 +137,9 @@ class FusedMLRenderer:
         # default stays fp32 atomics
         self.int_grad = False
         self.min_chunk = 512
+        # optional short first chunk per block (starts the scatter sooner):
+        # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
+        self.head_chunk = 0
         self.trace = False          # record HIP events around every launch
         self.events = {}
 
@@ -225,12 +228,15 @@ class FusedMLRenderer:
         (rn_bwd_plan), shared by the merged forward and backward."""
         w, L = self.ws, lib()
         self._min_chunk = min(self.min_chunk, self.max_chunk)
-        self._cap_chunks, self._chunks = w.chunk_list(self.max_chunk, self._min_chunk)
+        head_n = self.merged_blocks if self.head_chunk else 0
+        head = min(self.head_chunk, self.max_chunk)
+        self._cap_chunks, self._chunks = w.chunk_list(self.max_chunk, self._min_chunk, head_n)
         self._ev("bwd_plan", L.bwd_plan, w.counts.data_ptr(), w.offsets.data_ptr(),
                  w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, w.K,
-                 self.max_chunk, self._min_chunk, self._cap_chunks, w.mstart.data_ptr(),
-                 w.perm.data_ptr(), self._chunks.data_ptr(), w.queue.data_ptr(), st)
-        self._plan_key = (self.max_chunk, self._min_chunk)
+                 head_n, head, self.max_chunk, self._min_chunk, self._cap_chunks,
+                 w.mstart.data_ptr(), w.perm.data_ptr(), self._chunks.data_ptr(),
+                 w.queue.data_ptr(), st)
+        self._plan_key = (self.max_chunk, self._min_chunk, head_n, head)
 
     def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
         m, w, L = self.model, self.ws, lib()
@@ -251,8 +257,10 @@ class FusedMLRenderer:
                      w.feat.data_ptr() if self.feat_cache else None, self.fwd_blocks, st)
         elif self.merged_bwd:
             rows, scratch, park = w.bwd_scratch(self.merged_blocks, self.max_chunk)
-            if getattr(self, "_plan_key", None) != (self.max_chunk,
-                                                    min(self.min_chunk, self.max_chunk)):
+            if getattr(self, "_plan_key", None) != (
+                    self.max_chunk, min(self.min_chunk, self.max_chunk),
+                    self.merged_blocks if self.head_chunk else 0,
+                    min(self.head_chunk, self.max_chunk)):
                 self._plan(st)      # chunk sizes changed since the forward
             chunks = self._chunks
             ig = (None, None, None)
