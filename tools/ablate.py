@@ -1,7 +1,9 @@
 """Kernel ablation on the bench workload (dev tool): times field_bwd with parts
 switched off (rn_set_debug_flags) interleaved in one process (rule 24 of
 cdna_hip_programming.md §5.4).  bit0: no grid atomics, bit1: no dW, bit2: no
-grid scatter at all."""
+grid scatter at all, bit5 (32): rows staged but no walk (merged kernel).
+Token prefixes: none = merged backward, "s" = per-model backward, "i" =
+merged backward with integer accumulation, "f" = field_fwd."""
 import json
 import os
 import sys
@@ -45,8 +47,9 @@ def main():
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(int(f.lstrip("fs")))
+            L.set_debug_flags(int(f.lstrip("fsi")))
             r.merged_bwd = not f.startswith("s")
+            r.int_grad = f.startswith("i")
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             if f.startswith("f"):
