@@ -609,6 +609,7 @@ __device__ __forceinline__ void walk_end(const FieldArgs& a, const LvTab& sT, Sc
 struct Walk2 {
     uint32_t* ring;        // this wave's rings: [stream][3][W2_RING] words
     uint32_t head, tail;   // per lane: its stream's ring head / tail, in [0, W2_RING)
+    uint32_t pend;         // per lane: its stream's pending records (tail - head)
     uint32_t ex0, ex1, ey, ez, cur0, cur1;   // even-X / odd-X entries of the row
     float a00, a01, a10, a11;                // their accumulated feature gradients
     // integer mode: the two newest issues, checked for carries one issue late
@@ -617,7 +618,7 @@ struct Walk2 {
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
-    W.ring = ring; W.head = 0; W.tail = 0;
+    W.ring = ring; W.head = 0; W.tail = 0; W.pend = 0;
     W.ex0 = W2_NONE; W.ex1 = W2_NONE; W.ey = 0; W.ez = 0; W.cur0 = 0; W.cur1 = 0;
     W.a00 = W.a01 = W.a10 = W.a11 = 0.f;
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
@@ -684,7 +685,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         }
     }
     asm volatile("" ::: "memory");
-    if ((lane >> 2) == s) W.head = w2_wrap(W.head + cnt);
+    if ((lane >> 2) == s) { W.head = w2_wrap(W.head + cnt); W.pend -= cnt; }
 }
 
 // integer mode: settle the two outstanding issues (end of a chunk)
@@ -701,7 +702,7 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
                                             int dbg) {
     const bool lead = (rn_lane() & 3) == 0;
     for (;;) {
-        const uint32_t pend = W.tail >= W.head ? W.tail - W.head : W.tail + W2_RING - W.head;
+        const uint32_t pend = W.pend;
         uint64_t m = __builtin_amdgcn_ballot_w64(lead && pend > 0u && pend >= min_cnt);
         if (!m) break;
         while (m) {
@@ -741,7 +742,9 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint64_t 
         base[W2_RING + rec] = __float_as_uint(W.a10);
         base[2 * W2_RING + rec] = __float_as_uint(W.a11);
     }
-    W.tail = w2_wrap(W.tail + (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1)));
+    const uint32_t pushed = (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1));
+    W.tail = w2_wrap(W.tail + pushed);
+    W.pend += pushed;
 }
 
 __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& sT) {
@@ -798,12 +801,15 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
             W.a01 = (same0 ? W.a01 : 0.f) + w0 * gc.y;
             W.a10 = (same1 ? W.a10 : 0.f) + w1 * gc.x;
             W.a11 = (same1 ? W.a11 : 0.f) + w1 * gc.y;
-            // tcnn grid_index with the row part shared by the two entries
+            // tcnn grid_index with the row part shared by the two entries;
+            // branch-free dense / hashed select (the two levels of a wave differ)
             const uint32_t db = __umul24(Y, lc.res) + __umul24(Z, lc.res2);
             const uint32_t hb = (Y * 2654435761u) ^ (Z * 805459861u);
             const uint32_t d0 = X0 + db, d1 = X1 + db;
-            W.cur0 = lc.dense ? (d0 >= lc.hs ? d0 - lc.hs : d0) : ((X0 ^ hb) & (lc.hs - 1u));
-            W.cur1 = lc.dense ? (d1 >= lc.hs ? d1 - lc.hs : d1) : ((X1 ^ hb) & (lc.hs - 1u));
+            const uint32_t dm = lc.dense ? 0xffffffffu : 0u;
+            const uint32_t dd0 = min(d0, d0 - lc.hs), dd1 = min(d1, d1 - lc.hs);   // d < 2 hs
+            W.cur0 = (dd0 & dm) | ((X0 ^ hb) & (lc.hs - 1u) & ~dm);
+            W.cur1 = (dd1 & dm) | ((X1 ^ hb) & (lc.hs - 1u) & ~dm);
             W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
         }
         walk2_drain<IG>(W, 32u, grad_rs, G, dbg);
