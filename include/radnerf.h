@@ -191,7 +191,9 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: head_chunks
  * chunks of head_size merged samples (one per block, so the first scatter
  * starts early), then max_chunk up to 7/8 of the work, then min_chunk;
- * queue [3] i32 = bwd ticket, chunk count, fwd ticket).  cap_chunks must bound the chunk
+ * queue [3] i32 = bwd ticket, chunk count, fwd ticket; chunk_desc
+ * [cap_chunks][20] i32 = first ray, end ray, 2 pad, first sample [8], count [8]
+ * per model, read by the merged kernels with one 80-B load per ticket).  cap_chunks must bound the chunk
  * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2.
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
  * stages 144-B rows in its scratch slice (scratch: blocks x scratch_rows x 36
@@ -204,11 +206,11 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
                 int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
-                int32_t* queue, void* stream);
+                int32_t* chunk_desc, int32_t* queue, void* stream);
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
-                        const int32_t* chunk_first, int32_t* queue, int64_t n_rays,
+                        const int32_t* chunk_desc, int32_t* queue, int64_t n_rays,
                         int32_t n_models, int32_t max_samples,
                         const void* grid_f16, const uint32_t* level_offset,
                         const uint32_t* level_hsize, const uint32_t* level_res,
@@ -242,7 +244,7 @@ int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const fl
  * via ml_rendering.py:174-179).                                            */
 int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* chunk_first, int32_t* queue,
+                        const int32_t* offsets, const int32_t* chunk_desc, int32_t* queue,
                         int64_t n_rays, int32_t n_models, const void* grid_f16,
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,

@@ -1130,13 +1130,14 @@ k_field_bwd(FieldArgs a) {
 // to summation order); dW is identical per model.
 // ---------------------------------------------------------------------------
 #define MB_ROW 36          // scratch row floats: dE[32] | ux uy uz | pad
+#define CH_DESC 20         // chunk descriptor ints (80 B, 16-B aligned)
 #define MB_KMAX 8
 
 struct MergeArgs {
     const int32_t* offsets;  // [K][B] first sample of (model, ray)
     const int32_t* mstart;   // [B + 1] first merged position of ray r; [B] = total
     const int32_t* perm;     // [total] merged position -> sample index
-    const int32_t* chunk_first;  // [n_chunks + 1] first ray of each chunk; [n] = B
+    const int32_t* desc;     // [n_chunks][CH_DESC]: r0, r1, -, -, first sample [8], count [8]
     int32_t* queue;          // [0] bwd ticket, [1] n_chunks, [2] fwd ticket (rn_bwd_plan)
     float* scratch;          // [gridDim.x][rows_cap][MB_ROW]
     float* park;             // [gridDim.x][K][BWD_WAVES][32][64]
@@ -1203,29 +1204,31 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
     float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
     float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
     int n_local = 0;
+    int ticket = 0, n_chunks = 0;
+    if (threadIdx.x == 0) { n_chunks = m.queue[1]; ticket = atomicAdd(m.queue, 1); }
+    if (threadIdx.x < K) sCh[2 + 3 * MB_KMAX + threadIdx.x] = a.seg_base[threadIdx.x];
 
     for (;;) {
         __syncthreads();                         // previous chunk done with sCh / LDS
         if (threadIdx.x == 0) {
-            // next non-empty chunk of the plan (rn_bwd_plan's chunk list)
-            const int n_chunks = m.queue[1];
-            int r0 = B, r1 = B;
-            for (;;) {
-                const int ch = atomicAdd(m.queue, 1);
-                if (ch >= n_chunks) break;
-                r0 = m.chunk_first[ch]; r1 = m.chunk_first[ch + 1];
-                if (r1 > r0) break;
-                r0 = B;
+            // this chunk's descriptor (one 80-B load; its ticket was taken
+            // during the previous chunk) and the next chunk's ticket
+            const int ch = ticket;
+            ticket = atomicAdd(m.queue, 1);
+            int4 d[CH_DESC / 4];
+            if (ch < n_chunks) {
+#pragma unroll
+                for (int q = 0; q < CH_DESC / 4; ++q)
+                    d[q] = reinterpret_cast<const int4*>(m.desc + (size_t)ch * CH_DESC)[q];
             }
-            sCh[0] = r0; sCh[1] = r1;
+            const int32_t* di = reinterpret_cast<const int32_t*>(d);
+            sCh[0] = ch < n_chunks ? di[0] : B; sCh[1] = ch < n_chunks ? di[1] : B;
             int roff = 0;
             for (int k = 0; k < K; ++k) {
-                const int sb = a.seg_base[k];
-                const int a0 = r0 < B ? m.offsets[k * B + r0] : 0;
-                const int a1 = r1 < B ? m.offsets[k * B + r1] : sb + a.seg_count[k];
-                sCh[2 + k] = a0; sCh[2 + MB_KMAX + k] = r0 < B ? a1 - a0 : 0;
-                sCh[2 + 2 * MB_KMAX + k] = roff; sCh[2 + 3 * MB_KMAX + k] = sb;
-                roff += r0 < B ? a1 - a0 : 0;
+                const int nk = ch < n_chunks ? di[4 + MB_KMAX + k] : 0;
+                sCh[2 + k] = di[4 + k]; sCh[2 + MB_KMAX + k] = nk;
+                sCh[2 + 2 * MB_KMAX + k] = roff;
+                roff += nk;
             }
         }
         __syncthreads();
@@ -1371,23 +1374,24 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     const int waves = blockDim.x / RN_WAVE;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    int ticket = 0, n_chunks = 0;
+    if (threadIdx.x == 0) { n_chunks = m.queue[1]; ticket = atomicAdd(m.queue + 2, 1); }
     for (;;) {
         __syncthreads();
         if (threadIdx.x == 0) {
-            const int n_chunks = m.queue[1];
-            int r0 = B, r1 = B;
-            for (;;) {
-                const int ch = atomicAdd(m.queue + 2, 1);
-                if (ch >= n_chunks) break;
-                r0 = m.chunk_first[ch]; r1 = m.chunk_first[ch + 1];
-                if (r1 > r0) break;
-                r0 = B;
+            const int ch = ticket;
+            ticket = atomicAdd(m.queue + 2, 1);           // the next chunk's, ahead
+            int4 d[CH_DESC / 4];
+            if (ch < n_chunks) {
+#pragma unroll
+                for (int q = 0; q < CH_DESC / 4; ++q)
+                    d[q] = reinterpret_cast<const int4*>(m.desc + (size_t)ch * CH_DESC)[q];
             }
-            sCh[0] = r0;
+            const int32_t* di = reinterpret_cast<const int32_t*>(d);
+            sCh[0] = ch < n_chunks ? di[0] : B;
             for (int k = 0; k < K; ++k) {
-                const int a0 = r0 < B ? m.offsets[k * B + r0] : 0;
-                const int a1 = r1 < B ? m.offsets[k * B + r1] : a.seg_base[k] + a.seg_count[k];
-                sCh[2 + k] = a0; sCh[2 + FM_KMAX + k] = r0 < B ? a1 - a0 : 0;
+                sCh[2 + k] = di[4 + k];
+                sCh[2 + FM_KMAX + k] = ch < n_chunks ? di[4 + MB_KMAX + k] : 0;
             }
         }
         __syncthreads();
@@ -1553,23 +1557,45 @@ __device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head,
 }
 
 __global__ void __launch_bounds__(256)
-k_bwd_chunks(int B, const int32_t* __restrict__ mstart, int head_n, int head, int max_chunk,
+k_bwd_chunks(int B, int K, const int32_t* __restrict__ mstart,
+             const int32_t* __restrict__ offsets, const int32_t* __restrict__ seg_base,
+             const int32_t* __restrict__ seg_count, int head_n, int head, int max_chunk,
              int min_chunk, int cap_chunks, int32_t* __restrict__ chunk_first,
-             int32_t* __restrict__ queue) {
+             int32_t* __restrict__ desc, int32_t* __restrict__ queue) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = mstart[B];
     const ChunkPlan p = chunk_plan(total, head_n, head, max_chunk, min_chunk);
-    const int n = p.n;
-    if (c == 0) { queue[0] = 0; queue[1] = n < cap_chunks ? n : cap_chunks; queue[2] = 0; }
-    if (c > n || c > cap_chunks) return;
-    if (c == n || c == cap_chunks) { chunk_first[c] = B; return; }
-    const int bound = p.bound(c);
-    int lo = 0, hi = B;                       // first ray with mstart >= bound
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (mstart[mid] < bound) lo = mid + 1; else hi = mid;
+    const int n = min(p.n, cap_chunks);
+    if (c == 0) { queue[0] = 0; queue[1] = n; queue[2] = 0; }
+    if (c > n) return;
+    if (c == n) { chunk_first[c] = B; return; }
+    // first ray with mstart >= bound, for this chunk and the next
+    int first[2];
+    for (int e = 0; e < 2; ++e) {
+        if (c + e == n) { first[e] = B; continue; }
+        const int bound = p.bound(c + e);
+        int lo = 0, hi = B;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (mstart[mid] < bound) lo = mid + 1; else hi = mid;
+        }
+        first[e] = lo;
     }
-    chunk_first[c] = lo;
+    chunk_first[c] = first[0];
+    // descriptor: the chunk's sample range per model (the blocks read it with
+    // one 80-B load per ticket)
+    int32_t* d = desc + (size_t)c * CH_DESC;
+    const int r0 = first[0], r1 = first[1];
+    d[0] = r0; d[1] = r1; d[2] = 0; d[3] = 0;
+    for (int k = 0; k < MB_KMAX; ++k) {
+        int a0 = 0, cnt = 0;
+        if (k < K && r0 < B) {
+            a0 = offsets[k * B + r0];
+            const int a1 = r1 < B ? offsets[k * B + r1] : seg_base[k] + seg_count[k];
+            cnt = a1 - a0;
+        }
+        d[4 + k] = a0; d[4 + MB_KMAX + k] = cnt;
+    }
 }
 
 // dst[k][i] = idx[i] >= 0 ? f16(src[k][idx[i]]) : 0
@@ -1710,18 +1736,18 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
                 int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
-                int32_t* queue, void* stream) {
+                int32_t* chunk_desc, int32_t* queue, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX, "bad sizes");
     RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1 && head_chunks >= 0 &&
                  head_size >= 0 && head_size <= max_chunk, "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
-                 chunk_first && queue, "null pointer");
+                 chunk_first && chunk_desc && queue, "null pointer");
     k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
-        (int)n_rays, mstart, head_chunks, head_size, max_chunk, min_chunk, cap_chunks, chunk_first,
-        queue);
+        (int)n_rays, n_models, mstart, offsets, seg_base, seg_count, head_chunks, head_size,
+        max_chunk, min_chunk, cap_chunks, chunk_first, chunk_desc, queue);
     RN_CHECK_LAUNCH();
     return 0;
 }
@@ -1729,7 +1755,7 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
-                        const int32_t* chunk_first, int32_t* queue, int64_t n_rays,
+                        const int32_t* chunk_desc, int32_t* queue, int64_t n_rays,
                         int32_t n_models, int32_t max_samples,
                         const void* grid_f16, const uint32_t* level_offset,
                         const uint32_t* level_hsize, const uint32_t* level_res,
@@ -1745,7 +1771,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     RN_CHECK_ARG(scratch_rows >= (int64_t)max_chunk + (int64_t)n_models * max_samples,
                  "scratch_rows must be >= max_chunk + n_models * max_samples");
     RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets && mstart &&
-                 perm && chunk_first && queue && grid_f16 && level_offset && level_hsize && level_res &&
+                 perm && chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && dL_dsigma && dL_drgb && grid_grad &&
                  dw && scratch && park, "null pointer");
     FieldArgs a{};
@@ -1757,7 +1783,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
     a.seg_base = seg_base; a.seg_count = seg_count;
     MergeArgs m{};
-    m.offsets = offsets; m.mstart = mstart; m.perm = perm; m.chunk_first = chunk_first;
+    m.offsets = offsets; m.mstart = mstart; m.perm = perm; m.desc = chunk_desc;
     m.queue = queue;
     m.scratch = scratch; m.park = park;
     m.n_rays = (int)n_rays; m.n_models = n_models; m.rows_cap = (int)scratch_rows;
@@ -1789,7 +1815,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
 
 int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* chunk_first, int32_t* queue,
+                        const int32_t* offsets, const int32_t* chunk_desc, int32_t* queue,
                         int64_t n_rays, int32_t n_models, const void* grid_f16,
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,
@@ -1800,7 +1826,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  "bad sizes (n_models <= 4)");
     RN_CHECK_ARG(threads >= 64 && threads <= 1024 && threads % 64 == 0, "threads: 64..1024, waves");
     RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets &&
-                 chunk_first && queue && grid_f16 && level_offset && level_hsize && level_res &&
+                 chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && sigma && rgb, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
@@ -1810,7 +1836,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
     a.seg_base = seg_base; a.seg_count = seg_count;
     MergeArgs m{};
-    m.offsets = offsets; m.chunk_first = chunk_first; m.queue = queue;
+    m.offsets = offsets; m.desc = chunk_desc; m.queue = queue;
     m.n_rays = (int)n_rays; m.n_models = n_models;
     const size_t lds = (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
     hipStream_t st = (hipStream_t)stream;

@@ -44,7 +44,7 @@ SIGNATURES = {
     "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, I32, P],
     "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                      I32, P],
-    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P, P, P, P, P],
+    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
                             P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P],
     "rn_seed_scale": [P, P, I32, P, P, P, P, P, P],

@@ -70,6 +70,7 @@ class Workspace:
         cap = head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2
         if self._chunks is None or self._chunks.numel() < cap + 1:
             self._chunks = torch.empty(cap + 1, device=self.device, dtype=torch.int32)
+            self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
         return cap, self._chunks
 
     def bwd_scratch(self, blocks, max_chunk, max_samples=MAX_SAMPLES):
@@ -235,7 +236,7 @@ class FusedMLRenderer:
                  w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, w.K,
                  head_n, head, self.max_chunk, self._min_chunk, self._cap_chunks,
                  w.mstart.data_ptr(), w.perm.data_ptr(), self._chunks.data_ptr(),
-                 w.queue.data_ptr(), st)
+                 w._chunk_desc.data_ptr(), w.queue.data_ptr(), st)
         self._plan_key = (self.max_chunk, self._min_chunk, head_n, head)
 
     def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
@@ -248,7 +249,7 @@ class FusedMLRenderer:
         if fwd and self.merged_fwd:
             self._ev("field_fwd", L.field_fwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
-                     w.seg_count.data_ptr(), w.offsets.data_ptr(), self._chunks.data_ptr(),
+                     w.seg_count.data_ptr(), w.offsets.data_ptr(), w._chunk_desc.data_ptr(),
                      w.queue.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
                      w.rgb.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
                      self.merged_fwd_blocks, self.merged_fwd_threads, st)
@@ -279,7 +280,7 @@ class FusedMLRenderer:
             self._ev("field_bwd", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w.offsets.data_ptr(), w.mstart.data_ptr(),
-                     w.perm.data_ptr(), chunks.data_ptr(), w.queue.data_ptr(), w.B, m.size,
+                     w.perm.data_ptr(), w._chunk_desc.data_ptr(), w.queue.data_ptr(), w.B, m.size,
                      MAX_SAMPLES,
                      *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
                      dw.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
