@@ -209,7 +209,7 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                 int32_t* chunk_desc, int32_t* queue, void* stream);
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
+                        const int32_t* mstart, const int32_t* perm,
                         const int32_t* chunk_desc, int32_t* queue, int64_t n_rays,
                         int32_t n_models, int32_t max_samples,
                         const void* grid_f16, const uint32_t* level_offset,
@@ -244,7 +244,7 @@ int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const fl
  * via ml_rendering.py:174-179).                                            */
 int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* chunk_desc, int32_t* queue,
+                        const int32_t* chunk_desc, int32_t* queue,
                         int64_t n_rays, int32_t n_models, const void* grid_f16,
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,

@@ -1134,7 +1134,6 @@ k_field_bwd(FieldArgs a) {
 #define MB_KMAX 8
 
 struct MergeArgs {
-    const int32_t* offsets;  // [K][B] first sample of (model, ray)
     const int32_t* mstart;   // [B + 1] first merged position of ray r; [B] = total
     const int32_t* perm;     // [total] merged position -> sample index
     const int32_t* desc;     // [n_chunks][CH_DESC]: r0, r1, -, -, first sample [8], count [8]
@@ -1754,7 +1753,7 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
 
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* mstart, const int32_t* perm,
+                        const int32_t* mstart, const int32_t* perm,
                         const int32_t* chunk_desc, int32_t* queue, int64_t n_rays,
                         int32_t n_models, int32_t max_samples,
                         const void* grid_f16, const uint32_t* level_offset,
@@ -1770,7 +1769,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  max_samples >= 1 && max_chunk >= 1, "bad sizes");
     RN_CHECK_ARG(scratch_rows >= (int64_t)max_chunk + (int64_t)n_models * max_samples,
                  "scratch_rows must be >= max_chunk + n_models * max_samples");
-    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets && mstart &&
+    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && mstart &&
                  perm && chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && dL_dsigma && dL_drgb && grid_grad &&
                  dw && scratch && park, "null pointer");
@@ -1783,7 +1782,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
     a.seg_base = seg_base; a.seg_count = seg_count;
     MergeArgs m{};
-    m.offsets = offsets; m.mstart = mstart; m.perm = perm; m.desc = chunk_desc;
+    m.mstart = mstart; m.perm = perm; m.desc = chunk_desc;
     m.queue = queue;
     m.scratch = scratch; m.park = park;
     m.n_rays = (int)n_rays; m.n_models = n_models; m.rows_cap = (int)scratch_rows;
@@ -1815,7 +1814,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
 
 int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
-                        const int32_t* offsets, const int32_t* chunk_desc, int32_t* queue,
+                        const int32_t* chunk_desc, int32_t* queue,
                         int64_t n_rays, int32_t n_models, const void* grid_f16,
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,
@@ -1825,7 +1824,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && blocks >= 1,
                  "bad sizes (n_models <= 4)");
     RN_CHECK_ARG(threads >= 64 && threads <= 1024 && threads % 64 == 0, "threads: 64..1024, waves");
-    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && offsets &&
+    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count &&
                  chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && sigma && rgb, "null pointer");
     FieldArgs a{};
@@ -1836,7 +1835,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
     a.seg_base = seg_base; a.seg_count = seg_count;
     MergeArgs m{};
-    m.offsets = offsets; m.desc = chunk_desc; m.queue = queue;
+    m.desc = chunk_desc; m.queue = queue;
     m.n_rays = (int)n_rays; m.n_models = n_models;
     const size_t lds = (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
     hipStream_t st = (hipStream_t)stream;

@@ -249,7 +249,7 @@ class FusedMLRenderer:
         if fwd and self.merged_fwd:
             self._ev("field_fwd", L.field_fwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
-                     w.seg_count.data_ptr(), w.offsets.data_ptr(), w._chunk_desc.data_ptr(),
+                     w.seg_count.data_ptr(), w._chunk_desc.data_ptr(),
                      w.queue.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
                      w.rgb.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
                      self.merged_fwd_blocks, self.merged_fwd_threads, st)
@@ -279,7 +279,7 @@ class FusedMLRenderer:
                 ig = (lo.data_ptr(), carry.data_ptr(), scale.data_ptr())
             self._ev("field_bwd", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
-                     w.seg_count.data_ptr(), w.offsets.data_ptr(), w.mstart.data_ptr(),
+                     w.seg_count.data_ptr(), w.mstart.data_ptr(),
                      w.perm.data_ptr(), w._chunk_desc.data_ptr(), w.queue.data_ptr(), w.B, m.size,
                      MAX_SAMPLES,
                      *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
