@@ -192,10 +192,29 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
         for (int u = 0; u < 4; ++u) {
             const LvConst lc = lv_const(T, a.gm, lb + u);
             P[u] = level_pos(lc.sc, ux, uy, uz);
+            // tcnn grid_index of the lane's 4 corners (x = gx + h, rows (dy, dz)),
+            // the row part shared: dense levels x + y res + z res^2 (u24 exact,
+            // res <= 128), hashed x ^ y P1 ^ z P2 with (y+1) P1 = y P1 + P1.
+            // The level is wave-uniform, so only one branch runs.
+            const uint32_t x = P[u].gx + (uint32_t)h;
+            uint32_t idx[4];
+            if (lc.dense) {
+                const uint32_t b = x + __umul24(P[u].gy, lc.res) + __umul24(P[u].gz, lc.res2);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t d = b + ((r & 1) ? lc.res : 0u) + ((r >> 1) ? lc.res2 : 0u);
+                    idx[r] = d >= lc.hs ? d - lc.hs : d;
+                }
+            } else {
+                const uint32_t y0 = P[u].gy * 2654435761u, z0 = P[u].gz * 805459861u;
+                const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    idx[r] = (x ^ ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0)) & (lc.hs - 1u);
+            }
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const uint32_t idx = corner_index(lc, P[u], 2 * r + h);
-                const uint32_t ie = (a.dbg & 1024) ? (idx & 31u) : idx;   // ablation: 1 line per level
+                const uint32_t ie = (a.dbg & 1024) ? (idx[r] & 31u) : idx[r];   // ablation: 1 line per level
                 off[4 * u + r] = (valid && !(a.dbg & 128)) ? 4u * (lc.off + ie) : RN_OOB;
             }
         }
@@ -205,9 +224,13 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             float a0 = 0.f, a1 = 0.f;
+            // corner weight (wx * wy) * wz, tcnn's dimension order
+            const float wx = h ? P[u].fx : 1.0f - P[u].fx;
+            const float wy0 = 1.0f - P[u].fy, wz0 = 1.0f - P[u].fz;
+            const float wxy0 = wx * wy0, wxy1 = wx * P[u].fy;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float w = corner_weight(P[u], 2 * r + h);
+                const float w = ((r & 1) ? wxy1 : wxy0) * ((r >> 1) ? P[u].fz : wz0);
                 const uint32_t v = raw[4 * u + r];
                 a0 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu)), a0);
                 a1 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v >> 16)), a1);
@@ -340,7 +363,12 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
         if (CACHE == CACHE_WRITE && valid) { fc[0] = st.e0; fc[1] = st.e1; }
     }
     st.sh = sh_lane(dx, dy, dz, h);
-    mlp_forward(W, st);
+    if (a.dbg & 4096) {                 // ablation: no MLP (outputs are garbage)
+        st.out = rn_zero16(); st.g0 = 0.f;
+        asm volatile("" :: "v"(st.e0), "v"(st.e1), "v"(st.sh));
+    } else {
+        mlp_forward(W, st);
+    }
 }
 
 // encoding-cache slot of global sample s: 32-sample tiles of the sample
