@@ -61,7 +61,8 @@ def streams(ray, max_chunk, min_chunk=512, parts=8):
     return chunk * parts + part
 
 
-def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0, ent_per_seg=8):
+def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0, ent_per_seg=8,
+             sort_window=0):
     n = len(u)
     total = 0
     last = np.r_[sid[1:] != sid[:-1], True]                      # last sample of a stream
@@ -96,6 +97,24 @@ def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0
              else np.lexsort((k[:, 3], k[:, 2], k[:, 1], k[:, 0])))
         k, s = k[o], s[o]
         st = k[:, 0]
+        if sort_window:
+            # rings of sort_window records: when full, issue the 32 smallest segments
+            bnd = np.r_[np.flatnonzero(np.r_[True, st[1:] != st[:-1]]), len(st)]
+            req = 0
+            for a, b in zip(bnd[:-1], bnd[1:]):
+                pend = []
+                for x in s[a:b]:
+                    pend.append(x)
+                    if len(pend) >= sort_window:
+                        pend.sort()
+                        req += len(set(pend[:issue]))
+                        pend = pend[issue:]
+                while pend:
+                    pend.sort()
+                    req += len(set(pend[:issue]))
+                    pend = pend[issue:]
+            total += req
+            continue
         if cut_min:
             # cut each instruction at a segment boundary (largest k in [cut_min, issue])
             grp = np.empty(len(st), np.int64)
@@ -132,11 +151,12 @@ def main():
     lane_major = len(sys.argv) > 5 and sys.argv[5] == "lane"
     cut_min = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     eps = int(sys.argv[7]) if len(sys.argv) > 7 else 8
+    sw = int(sys.argv[8]) if len(sys.argv) > 8 else 0
     u, ray, lv = merged_samples(B)
     sid = streams(ray, mc, parts=parts)
     print(f"B {B} samples {len(u)} max_chunk {mc} issue {issue} parts {parts} "
           f"{'lane' if lane_major else 'slot'}-major: "
-          f"requests/sample {requests(u, lv, sid, issue, lane_major=lane_major, cut_min=cut_min, ent_per_seg=eps):.2f} (cut_min {cut_min}, entries/segment {eps})")
+          f"requests/sample {requests(u, lv, sid, issue, lane_major=lane_major, cut_min=cut_min, ent_per_seg=eps, sort_window=sw):.2f} (cut_min {cut_min}, entries/segment {eps}, sort window {sw})")
 
 
 if __name__ == "__main__":
