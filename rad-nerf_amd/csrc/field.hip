@@ -1,11 +1,11 @@
 // Fused Rad-NeRF field for gfx950: shared multiresolution hash grid + per
-// sub-NeRF geo/rgb MLPs, forward and backward, one kernel each.
+// sub-NeRF geo/rgb MLPs, forward and backward.
 //
 // Reference (behaviour): models/networks.py:291-328 (MNGP.density/forward),
 // :229-289 (tcnn Grid/Hash encoding L=16 F=2 T=2^19 N_min=16, SH degree 4,
 // FullyFusedMLP geo 32->64->17, rgb 32->64->64->3 Sigmoid), custom_functions.py
 // :162-173 (TruncExp).  tcnn itself is an absent third-party dependency; the
-// encoding/SH/MLP semantics restated here are listed in DESIGN.md §field.
+// encoding/SH/MLP semantics restated here are listed in DESIGN.md §2.
 //
 // Work decomposition: one wave = 32 samples.  Lane (c = lane&31, h = lane>>5)
 // owns sample c and 8 of the 16 hash levels, {2h,2h+1,4+2h,5+2h,8+2h,...}: the
@@ -13,12 +13,20 @@
 // the accumulator of the last backward layer, so the encoding enters and
 // leaves the MFMA chain without any data movement.
 //
-// Backward: recompute the forward in registers, run the dX chain on MFMA,
-// stage (dY, X) per layer through a wave-private LDS image to form
-// dW = dY . X^T with the samples as contraction index (MFMA again), reduce dW
-// over the whole persistent block in LDS (ds_add_f32), and scatter the hash
-// grid gradient with fp32 atomics laid out 4 samples x 8 corners x 2 features
-// per wave instruction so adjacent corners of one sample share 64-B lines.
+// Kernels:
+//  * k_field_fwd / k_field_bwd: one sub-NeRF per blockIdx.y (the drop-in
+//    path, one model at a time like the reference).
+//  * k_bwd_plan + k_bwd_chunks: merged (ray, t) order of the K models'
+//    samples and a chunk schedule of whole rays.
+//  * k_field_fwd_merged: the K models' tiles of a chunk interleaved on one
+//    CU (their corners share L1 lines).
+//  * k_field_bwd_merged: per chunk, the MLP backward model by model, then the
+//    hash-grid gradient of all K models scattered in merged per-ray order
+//    (row-lane walk + per-stream rings of fp32 atomics; optionally exact
+//    integer accumulation).
+// Backward MLP: recompute the forward from the encoding cache, run the dX
+// chain on MFMA, and form dW = dY . X^T block-cooperatively from sample-major
+// LDS images (MFMA again), held in registers across windows.
 #include "rn_mlp.h"
 #pragma clang fp contract(off)
 
