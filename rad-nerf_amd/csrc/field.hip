@@ -108,6 +108,7 @@ struct LvTab {
     uint32_t off[RN_L];
     uint32_t hs[RN_L];
     uint32_t res[RN_L];
+    uint32_t res2[RN_L];
     float sc[RN_L];
 };
 
@@ -115,6 +116,7 @@ __device__ __forceinline__ void lv_stage(LvTab& t, const GridMeta& gm) {
     const int i = threadIdx.x;
     if (i < RN_L) {
         t.off[i] = gm.offset[i]; t.hs[i] = gm.hsize[i]; t.res[i] = gm.res[i]; t.sc[i] = gm.scale[i];
+        t.res2[i] = gm.res[i] * gm.res[i];
     }
 }
 
@@ -127,7 +129,7 @@ struct LvConst {
 
 __device__ __forceinline__ LvConst lv_const(const LvTab& T, const GridMeta& gm, int l) {
     LvConst c;
-    c.off = T.off[l]; c.hs = T.hs[l]; c.res = T.res[l]; c.res2 = c.res * c.res; c.sc = T.sc[l];
+    c.off = T.off[l]; c.hs = T.hs[l]; c.res = T.res[l]; c.res2 = T.res2[l]; c.sc = T.sc[l];
     c.dense = (gm.dense_mask >> l) & 1u;
     return c;
 }
@@ -180,9 +182,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rn_rsrc(const void* p, uint32_
 // x-neighbours of a row for 32 samples: both sit in one 128-B line almost
 // always, and the cost of a gather instruction on gfx950 is its number of
 // distinct lines (measured: the same stream with every lane of an instruction
-// in one line runs as fast as with no memory access at all; tools/ablate.py
+// in one line runs as fast as with no memory access at all, r01 ablation
 // f1024).  28 lines/sample instead of 53 with one corner of two levels per
-// instruction (tools/atomic_sim.py's replay of the bench samples).
+// instruction (tools/atomic_sim.py's replay of the bench samples).  A lane
+// per (sample, level) with all 8 corners does 40 % less VALU work (position
+// and row hash once per sample) but is 5 % slower: its instructions touch
+// twice the lines (profiles/r01/ablate_fwd_levelsplit.json).
 // The two x-halves of each level are summed across the wave halves with
 // v_permlane32_swap (x0 half first, so both lanes hold the same value); each
 // lane keeps the 8 levels of its B-fragment rows (lane_level).
@@ -192,6 +197,7 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
                                             __amdgpu_buffer_rsrc_t rs, int h, float ux, float uy,
                                             float uz, bool valid, half8& e0, half8& e1) {
     float f[16];
+    const bool load = valid && !(a.dbg & 128);
 #pragma unroll
     for (int lb = 0; lb < RN_L; lb += 4) {
         LevelPos P[4];
@@ -220,11 +226,11 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
                 for (int r = 0; r < 4; ++r)
                     idx[r] = (x ^ ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0)) & (lc.hs - 1u);
             }
+            // one v_add_lshl per corner; invalid lanes start past num_records
+            // (the table is < 2^31 B)
+            const uint32_t ob = load ? lc.off : (RN_OOB >> 2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const uint32_t ie = (a.dbg & 1024) ? (idx[r] & 31u) : idx[r];   // ablation: 1 line per level
-                off[4 * u + r] = (valid && !(a.dbg & 128)) ? 4u * (lc.off + ie) : RN_OOB;
-            }
+            for (int r = 0; r < 4; ++r) off[4 * u + r] = (ob + idx[r]) << 2;
         }
         uint32_t raw[16];
 #pragma unroll

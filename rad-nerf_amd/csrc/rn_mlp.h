@@ -52,10 +52,15 @@ template <bool RELU>
 __device__ __forceinline__ void rn_acc_to_frags(const f32x16& acc, half8& f0, half8& f1) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        float a = acc[j], b = acc[8 + j];
-        if (RELU) { a = fmaxf(a, 0.f); b = fmaxf(b, 0.f); }
-        f0[j] = (rn_half)a;
-        f1[j] = (rn_half)b;
+        f0[j] = (rn_half)acc[j];
+        f1[j] = (rn_half)acc[8 + j];
+    }
+    // ReLU after the f16 rounding (same values: rounding is monotone and keeps
+    // the sign): packed maxes on canonical operands, 1 op per 2 elements
+    // instead of canonicalize + max per element
+    if (RELU) {
+        f0 = __builtin_elementwise_max(f0, rn_zero8());
+        f1 = __builtin_elementwise_max(f1, rn_zero8());
     }
 }
 
