@@ -70,6 +70,9 @@ def parse():
                     help="merged backward: largest chunk of merged samples per queue grab")
     ap.add_argument("--head-chunk", type=int, default=0,
                     help="merged passes: first chunk per block (0 = none)")
+    ap.add_argument("--pinned", action="store_true",
+                    help="sub-NeRF-per-GPU layout (SURVEY.md §8(e) C5): rank r renders ALL rays "
+                         "for its K/N sub-NeRFs, per-ray outputs all-gathered (strong scaling)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
                          "multi-rank path on one GPU")
@@ -98,15 +101,21 @@ def main():
     with torch.no_grad():
         for i in range(K):
             getattr(model, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
-    o_np, d_np = S.rays(B, scale, seed=1000 * rank)
+    # data parallel: every rank its own rays; pinned: the same rays on every rank
+    rs = 0 if args.pinned else rank
+    o_np, d_np = S.rays(B, scale, seed=1000 * rs)
     rays_o = torch.from_numpy(o_np).to(dev)
     rays_d = torch.from_numpy(d_np).to(dev)
-    noises = [torch.from_numpy(S.noise(K, B, seed=2 + 7919 * rank + i)).to(dev) for i in range(4)]
-    seeds_np = S.loss_seeds(B, K, seed=4 + rank)
+    noises = [torch.from_numpy(S.noise(K, B, seed=2 + 7919 * rs + i)).to(dev) for i in range(4)]
+    seeds_np = S.loss_seeds(B, K, seed=4 + rs)
     g_rgb, g_op, g_depth = (torch.from_numpy(s).to(dev) for s in seeds_np)
     bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
 
-    r = FusedMLRenderer(model, gate, B)
+    if args.pinned:
+        from radnerf_amd.pinned import PinnedMLRenderer
+        r = PinnedMLRenderer(model, gate, B)
+    else:
+        r = FusedMLRenderer(model, gate, B)
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk
@@ -120,7 +129,7 @@ def main():
         r.backward(rays_o, rays_d, rays_d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4,
                    grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
         if world > 1:
-            ar.reduce()
+            ar.reduce(average=not args.pinned)   # pinned: partial gradients add up
 
     for i in range(args.warmup):
         step(i)
@@ -178,7 +187,7 @@ def main():
             r.train_step(rays_o, rays_d, rays_d, tgt, noises[i % 4], bg, 1e-3, 1e-2, 5e-2,
                          1e-4, esf, ar.views[0], ar.views[1], ar.views[2])
             if world > 1:
-                ar.reduce()
+                ar.reduce(average=not args.pinned)
             opt.step()
 
         for i in range(2):
@@ -250,17 +259,25 @@ def main():
         rgb_linf, cpu_base = oracle_legs(args, model, gate, bits, o_np, d_np, noises[0], r,
                                          rays_o, rays_d, bg, esf, scale, seeds_np)
 
+    if args.pinned:
+        workload = (f"Rad-NeRF train_ml.py K={K} gate=ray, sub-NeRFs pinned {K // world} per GPU, "
+                    f"B={B} rays on every GPU, scale={scale}, random 128^3 occupancy "
+                    f"p={args.occupancy:.2f}")
+    else:
+        workload = (f"C3 Rad-NeRF train_ml.py K={K} gate=ray B={B}/GPU scale={scale}, "
+                    f"random 128^3 occupancy p={args.occupancy:.2f}")
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
-               "scaling": "weak", "vs_baseline": None, "dtype": "f16/f32",
+               "scaling": "strong" if args.pinned else "weak", "vs_baseline": None,
+               "dtype": "f16/f32",
                "data": "synthetic",
-               "config": {"workload": "C3 Rad-NeRF train_ml.py K=2 gate=ray B=8192/GPU "
-                                      "scale=0.5, random 128^3 occupancy p=%.2f" % args.occupancy,
+               "config": {"workload": workload,
                           "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
-                          "global_batch": B * world, "parallelism": f"dp{world}"},
+                          "global_batch": B if args.pinned else B * world,
+                          "parallelism": f"pinned{world}" if args.pinned else f"dp{world}"},
                "roofline": roofline, "cpu_baseline": cpu_base,
                "rgb_linf_vs_ref": rgb_linf,
                "forward_only": fwd_only,

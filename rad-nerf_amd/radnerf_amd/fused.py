@@ -141,6 +141,8 @@ class FusedMLRenderer:
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
         self.head_chunk = 0
+        # gate backward on this process (pinned.PinnedMLRenderer: rank 0 only)
+        self.gate_grad_here = True
         self.trace = False          # record HIP events around every launch
         self.events = {}
 
@@ -179,16 +181,16 @@ class FusedMLRenderer:
     def forward(self, rays_o, rays_d, gate_in2, noise, bg, T_threshold=1e-4,
                 exp_step_factor=0.0):
         m, g, w, L = self.model, self.gate, self.ws, lib()
-        B, K = rays_o.shape[0], m.size
+        B, K, G = rays_o.shape[0], m.size, g.out_dim     # K rendered here, G gated
         assert B == w.B and noise.shape == (K, B)
         st = _stream(rays_o.device)
-        out_gate = torch.empty(B, K, device=rays_o.device)
-        imp = torch.zeros(K, device=rays_o.device)
+        out_gate = torch.empty(B, G, device=rays_o.device)
+        imp = torch.zeros(G, device=rays_o.device)
         side = self._side(rays_o.device)
         main = torch.cuda.current_stream(rays_o.device)
         frags = g.packed_frags()          # (re)packed on the main stream
         side.wait_stream(main)
-        self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
+        self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
                  frags.data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
                  max(1, min(256, (B + 127) // 128)), side.cuda_stream, stream=side)
         bits = self.bitfields()
@@ -213,16 +215,28 @@ class FusedMLRenderer:
                           w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
                           float(T_threshold), w.used.data_ptr(), w.opacity_k.data_ptr(),
                           w.depth_k.data_ptr(), w.rgb_k.data_ptr(), w.ws.data_ptr(), st)
+        # per-ray outputs of all G gated sub-NeRFs (here: the K rendered ones;
+        # pinned.PinnedMLRenderer gathers them from every rank)
+        ok, dk, rk = self._all_model_outputs()
         rgb = torch.empty(B, 3, device=rays_o.device)
         opacity = torch.empty(B, device=rays_o.device)
-        depth = torch.empty(B, K, device=rays_o.device)
+        depth = torch.empty(B, G, device=rays_o.device)
         main.wait_stream(side)            # gate output joins here
         out_gate.record_stream(side)
         imp.record_stream(side)
-        self._ev("combine_fw", L.ml_combine_fw, out_gate.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
-                        w.rgb_k.data_ptr(), bg.data_ptr(), B, K, rgb.data_ptr(),
+        self._ev("combine_fw", L.ml_combine_fw, out_gate.data_ptr(), ok.data_ptr(), dk.data_ptr(),
+                        rk.data_ptr(), bg.data_ptr(), B, G, rgb.data_ptr(),
                         opacity.data_ptr(), depth.data_ptr(), st)
         return rgb, opacity, depth, out_gate, imp
+
+    def _all_model_outputs(self):
+        """(opacity, depth, rgb) per (sub-NeRF, ray) of every gated sub-NeRF."""
+        w = self.ws
+        return w.opacity_k, w.depth_k, w.rgb_k
+
+    def _local_cols(self, x):
+        """Columns of a (B, G) per-ray tensor that belong to the rendered sub-NeRFs."""
+        return x
 
     def _plan(self, st):
         """Merged (ray, t) order + chunk schedule of this step's samples
@@ -301,18 +315,22 @@ class FusedMLRenderer:
         """Accumulates into grid_grad / mlp_grad / gate_grad (zero-initialised
         by the caller or allocated here) and returns them."""
         m, g, w, L = self.model, self.gate, self.ws, lib()
-        B, K = rays_o.shape[0], m.size
+        B, K, G = rays_o.shape[0], m.size, g.out_dim
         dev = rays_o.device
         st = _stream(dev)
         grid_grad = torch.zeros_like(m.xyz_encoder.params) if grid_grad is None else grid_grad
         mlp_grad = torch.zeros_like(m.mlp_params) if mlp_grad is None else mlp_grad
         gate_grad = torch.zeros_like(g.params) if gate_grad is None else gate_grad
-        self._ev("combine_bw", L.ml_combine_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(), w.opacity_k.data_ptr(),
-                        w.rgb_k.data_ptr(), bg.data_ptr(), B, K, w.dgate.data_ptr(), st)
+        ok, _, rk = self._all_model_outputs()
+        dgate = self._dgate(B, G)
+        self._ev("combine_bw", L.ml_combine_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
+                 ok.data_ptr(), rk.data_ptr(), bg.data_ptr(), B, G, dgate.data_ptr(), st)
         if dL_dgate_ext is not None:
-            w.dgate.add_(dL_dgate_ext)
+            dgate.add_(dL_dgate_ext)
+        gate_k = self._local_cols(gate)
+        ddepth_k = None if dL_ddepth is None else self._local_cols(dL_ddepth)
         self._ev("composite_bw", L.ml_composite_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
-                          None if dL_ddepth is None else dL_ddepth.data_ptr(), gate.data_ptr(),
+                          None if ddepth_k is None else ddepth_k.data_ptr(), gate_k.data_ptr(),
                           bg.data_ptr(), w.sigma.data_ptr(), w.rgb.data_ptr(),
                           w.deltas.data_ptr(), w.ts.data_ptr(), w.counts.data_ptr(),
                           w.offsets.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
@@ -321,17 +339,21 @@ class FusedMLRenderer:
         # gate backward beside field_bwd: it only needs dL/dgate (combine_bw)
         side = self._side(dev)
         main = torch.cuda.current_stream(dev)
-        frags = g.packed_frags()
-        side.wait_stream(main)
-        self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, K,
-                 frags.data_ptr(), w.dgate.data_ptr(), gate_grad.data_ptr(),
-                 gate_grad.numel(), max(1, min(128, (B + 127) // 128)), side.cuda_stream,
-                 stream=side)
+        if self.gate_grad_here:
+            frags = g.packed_frags()
+            side.wait_stream(main)
+            self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
+                     frags.data_ptr(), dgate.data_ptr(), gate_grad.data_ptr(),
+                     gate_grad.numel(), max(1, min(128, (B + 127) // 128)), side.cuda_stream,
+                     stream=side)
         self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
-        main.wait_stream(side)
-        gate_grad.record_stream(side)
+        if self.gate_grad_here:
+            main.wait_stream(side)
+            gate_grad.record_stream(side)
         return grid_grad, mlp_grad, gate_grad
 
+    def _dgate(self, B, G):
+        return self.ws.dgate
 
     # --------------------------------------------------------------- train step
     def train_step(self, rays_o, rays_d, gate_in2, target_rgb, noise, bg, lambda_opacity=1e-3,
