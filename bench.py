@@ -135,7 +135,9 @@ def main():
         step(i)
     torch.cuda.synchronize()
     samples_acc.zero_()
-    r.trace = True
+    # timed region: HIP events only around the roofline kernel (an event pair
+    # per launch costs ~5 us of queue time; all twelve would add ~2.5 %)
+    r.trace = {"field_bwd"}
     r.events = {}
     if world > 1:
         dist.barrier()
@@ -147,8 +149,18 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    bwd_live = r.kernel_times_ms()["field_bwd"]
+    # per-kernel breakdown: the same steps again with every launch traced
+    # (after the timed region; not part of `value`)
+    r.trace = True
+    r.events = {}
+    saved = samples_acc.clone()
+    for i in range(args.steps):
+        step(i)
+    samples_acc.copy_(saved)
     r.trace = False
     kt = r.kernel_times_ms()
+    kt["field_bwd"] = bwd_live
 
     # forward-only rate (north_star's forward target), timed after the headline
     # region with the same barrier/sync bracketing; not part of `value`

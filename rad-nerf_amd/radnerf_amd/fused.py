@@ -141,15 +141,19 @@ class FusedMLRenderer:
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
         self.head_chunk = 0
-        # gate backward on this process (pinned.PinnedMLRenderer: rank 0 only)
+        # gate backward on this process (pinned.PinnedMLRenderer: rank 0 only),
+        # and where: "field" side stream beside field_bwd, "early" side stream
+        # beside composite_bw, "main" in line before field_bwd
         self.gate_grad_here = True
-        self.trace = False          # record HIP events around every launch
+        self.gate_bwd_at = "field"
+        # record HIP events around every launch (True) or the named ones (a set)
+        self.trace = False
         self.events = {}
 
     def _ev(self, name, L_call, *args, stream=None):
-        """Launch through librn; with tracing on, bracket it with events on the
-        launch stream (bench.py's per-kernel timing)."""
-        if not self.trace:
+        """Launch through librn; with tracing on (for this kernel), bracket it
+        with events on the launch stream (bench.py's per-kernel timing)."""
+        if not self.trace or (self.trace is not True and name not in self.trace):
             return L_call(*args)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record(stream)
@@ -327,6 +331,22 @@ class FusedMLRenderer:
                  ok.data_ptr(), rk.data_ptr(), bg.data_ptr(), B, G, dgate.data_ptr(), st)
         if dL_dgate_ext is not None:
             dgate.add_(dL_dgate_ext)
+        side = self._side(dev)
+        main = torch.cuda.current_stream(dev)
+
+        def gate_bwd(stream):
+            frags = g.packed_frags()
+            if stream is side:
+                side.wait_stream(main)
+            self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
+                     frags.data_ptr(), dgate.data_ptr(), gate_grad.data_ptr(),
+                     gate_grad.numel(), max(1, min(128, (B + 127) // 128)), stream.cuda_stream,
+                     stream=stream)
+
+        # gate backward: it only needs dL/dgate (combine_bw)
+        gate_at = self.gate_bwd_at if self.gate_grad_here else None
+        if gate_at == "early":          # side stream, beside composite_bw
+            gate_bwd(side)
         gate_k = self._local_cols(gate)
         ddepth_k = None if dL_ddepth is None else self._local_cols(dL_ddepth)
         self._ev("composite_bw", L.ml_composite_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
@@ -336,18 +356,12 @@ class FusedMLRenderer:
                           w.offsets.data_ptr(), w.opacity_k.data_ptr(), w.depth_k.data_ptr(),
                           w.rgb_k.data_ptr(), B, K, float(T_threshold), w.dsigma.data_ptr(),
                           w.drgb.data_ptr(), st)
-        # gate backward beside field_bwd: it only needs dL/dgate (combine_bw)
-        side = self._side(dev)
-        main = torch.cuda.current_stream(dev)
-        if self.gate_grad_here:
-            frags = g.packed_frags()
-            side.wait_stream(main)
-            self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
-                     frags.data_ptr(), dgate.data_ptr(), gate_grad.data_ptr(),
-                     gate_grad.numel(), max(1, min(128, (B + 127) // 128)), side.cuda_stream,
-                     stream=side)
+        if gate_at == "field":          # side stream, beside field_bwd
+            gate_bwd(side)
+        elif gate_at == "main":         # in line, before field_bwd
+            gate_bwd(main)
         self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
-        if self.gate_grad_here:
+        if gate_at in ("early", "field"):
             main.wait_stream(side)
             gate_grad.record_stream(side)
         return grid_grad, mlp_grad, gate_grad
