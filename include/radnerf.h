@@ -241,7 +241,10 @@ int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const fl
  * [2] is the forward's ticket) and evaluate the models' tiles of a chunk
  * interleaved, so the K sub-NeRFs' samples of one ray share cached grid
  * lines.  Replaces the per-sub-NeRF MNGP forward (models/networks.py:300-328
- * via ml_rendering.py:174-179).                                            */
+ * via ml_rendering.py:174-179).  With mstart and perm (rn_bwd_plan's merged
+ * order) and feat_cache, each chunk is first encoded in merged (ray, t, model)
+ * order into feat_cache, then the per-model MLP tiles read it back (NULL,
+ * NULL: every tile encodes its own samples).  Outputs are identical.       */
 int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* chunk_desc, int32_t* queue,
@@ -249,8 +252,8 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,
                         const float* xyz_min, const float* extent, const void* frags,
-                        float* sigma, float* rgb, void* feat_cache, int32_t blocks,
-                        int32_t threads, void* stream);
+                        float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
+                        const int32_t* perm, int32_t blocks, int32_t threads, void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------
  * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)

@@ -351,7 +351,8 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
 
-enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2 };
+enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2,
+       CACHE_READ_NT = 3 };   // READ past L1: written by other waves of this kernel
 
 // forward of one 32-sample tile for the lanes' samples `s` (valid lanes only
 // load); fc: this lane's encoding-cache slot (CACHE_WRITE writes it on every
@@ -366,11 +367,15 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-    if (CACHE == CACHE_READ) {
+    if (CACHE == CACHE_READ || CACHE == CACHE_READ_NT) {
         // lanes past the segment end (the backward walks whole 8-tile
         // iterations) were never written: zero encoding, as the gather path
         st.e0 = rn_zero8(); st.e1 = rn_zero8();
-        if (valid) { st.e0 = fc[0]; st.e1 = fc[1]; }
+        if (valid && CACHE == CACHE_READ) { st.e0 = fc[0]; st.e1 = fc[1]; }
+        if (valid && CACHE == CACHE_READ_NT) {
+            st.e0 = __builtin_nontemporal_load(fc);
+            st.e1 = __builtin_nontemporal_load(fc + 1);
+        }
     } else {
         if (a.dbg & 256) { st.e0 = rn_zero8(); st.e1 = rn_zero8(); asm volatile("" :: "v"(ux), "v"(uy), "v"(uz)); }
         else encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
@@ -1400,7 +1405,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
 // ---------------------------------------------------------------------------
 #define FM_KMAX 4
 
-template <int CACHE>
+template <int CACHE, bool ENC_M>
 __global__ void __launch_bounds__(1024)
 k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
@@ -1430,6 +1435,7 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
             }
             const int32_t* di = reinterpret_cast<const int32_t*>(d);
             sCh[0] = ch < n_chunks ? di[0] : B;
+            sCh[1] = ch < n_chunks ? di[1] : B;
             for (int k = 0; k < K; ++k) {
                 sCh[2 + k] = di[4 + k];
                 sCh[2 + FM_KMAX + k] = ch < n_chunks ? di[4 + MB_KMAX + k] : 0;
@@ -1437,6 +1443,28 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
         }
         __syncthreads();
         if (sCh[0] >= B) break;
+        if (ENC_M) {
+            // 1. encode the chunk in merged (ray, t, model) order: a tile mixes
+            // the sub-NeRFs of one ray stretch, so its corners share more lines
+            // (tools/fwd_lines_sim.py: 20.9 vs 28.2 lines per sample); the
+            // encodings go to the cache the MLP tiles and the backward read
+            const int p_base = m.mstart[sCh[0]], n_p = m.mstart[sCh[1]] - p_base;
+            for (int u = wid; u * 32 < n_p; u += waves) {
+                const int q = u * 32 + c;
+                const bool valid = q < n_p;
+                const int64_t s = m.perm[p_base + (valid ? q : 0)];
+                float x, y, z, dx, dy, dz;
+                load_sample<1>(a, s, x, y, z, dx, dy, dz);
+                const float ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
+                const float uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
+                const float uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
+                half8 e0, e1;
+                encode_lane(a, sT, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, e0, e1);
+                if (valid) { half8* fc = cache_slot(a, s); fc[0] = e0; fc[1] = e1; }
+            }
+            __syncthreads();
+        }
+        // 2. (or only) the per-model tiles, interleaved across models
         int max_t = 0;
         for (int k = 0; k < K; ++k) max_t = max(max_t, (sCh[2 + FM_KMAX + k] + 31) >> 5);
         for (int u = wid; u < max_t * K; u += waves) {
@@ -1449,9 +1477,10 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
             const int64_t s = sCh[2 + k] + (valid ? i : 0);
             FwdState st;
             float ux, uy, uz;
-            tile_forward_s<1, CACHE>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
-                                     valid, CACHE == CACHE_WRITE ? cache_slot(a, s) : nullptr,
-                                     st, ux, uy, uz);
+            constexpr int TC = ENC_M ? CACHE_READ_NT : CACHE;
+            tile_forward_s<1, TC>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
+                                  valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
+                                  st, ux, uy, uz);
             if (valid && h == 0) {
                 a.sigma[s] = expf(st.g0);
                 a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
@@ -1861,14 +1890,16 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         const uint32_t* level_offset, const uint32_t* level_hsize,
                         const uint32_t* level_res, const float* level_scale,
                         const float* xyz_min, const float* extent, const void* frags,
-                        float* sigma, float* rgb, void* feat_cache, int32_t blocks,
-                        int32_t threads, void* stream) {
+                        float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
+                        const int32_t* perm, int32_t blocks, int32_t threads, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && blocks >= 1,
                  "bad sizes (n_models <= 4)");
     RN_CHECK_ARG(threads >= 64 && threads <= 1024 && threads % 64 == 0, "threads: 64..1024, waves");
     RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count &&
                  chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && sigma && rgb, "null pointer");
+    RN_CHECK_ARG(!(mstart || perm) || (mstart && perm && feat_cache),
+                 "merged-order encoding needs mstart, perm and the encoding cache");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.dbg = g_field_dbg;
@@ -1878,6 +1909,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     a.seg_base = seg_base; a.seg_count = seg_count;
     MergeArgs m{};
     m.desc = chunk_desc; m.queue = queue;
+    m.mstart = mstart; m.perm = perm;
     m.n_rays = (int)n_rays; m.n_models = n_models;
     const size_t lds = (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
     hipStream_t st = (hipStream_t)stream;
@@ -1885,8 +1917,9 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         rn_set_error("%s: ticket reset failed", __func__);
         return 2;
     }
-    if (feat_cache) k_field_fwd_merged<CACHE_WRITE><<<blocks, threads, lds, st>>>(a, m);
-    else k_field_fwd_merged<CACHE_NONE><<<blocks, threads, lds, st>>>(a, m);
+    if (mstart) k_field_fwd_merged<CACHE_WRITE, true><<<blocks, threads, lds, st>>>(a, m);
+    else if (feat_cache) k_field_fwd_merged<CACHE_WRITE, false><<<blocks, threads, lds, st>>>(a, m);
+    else k_field_fwd_merged<CACHE_NONE, false><<<blocks, threads, lds, st>>>(a, m);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -124,6 +124,10 @@ class FusedMLRenderer:
         # model's corners hit lines the first fetched: C3 1.12 ms vs 1.30 ms
         # (tools/fwd_blocks_sweep.py; 2 blocks per CU 1.17, 3 x 4 waves 1.35)
         self.merged_fwd = model.size <= 4
+        # merged forward: encode each chunk in merged (ray, t, model) order
+        # first (tiles mixing the sub-NeRFs of a ray stretch share more grid
+        # lines), then the per-model MLP tiles read the encoding cache
+        self.merged_encode = True
         self.merged_fwd_blocks = 256
         self.merged_fwd_threads = 512
         self.merged_blocks = 256
@@ -270,6 +274,8 @@ class FusedMLRenderer:
                      w.seg_count.data_ptr(), w._chunk_desc.data_ptr(),
                      w.queue.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
                      w.rgb.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
+                     *((w.mstart.data_ptr(), w.perm.data_ptr())
+                       if self.feat_cache and self.merged_encode else (None, None)),
                      self.merged_fwd_blocks, self.merged_fwd_threads, st)
         elif fwd:
             self._ev("field_fwd", L.field_fwd, *common, w.sigma.data_ptr(), w.rgb.data_ptr(),

@@ -191,16 +191,17 @@ def test_merged_backward_chunking(cuda):
 
 @pytest.mark.parametrize("B,K,scale", [(4096, 2, 0.5), (1024, 4, 16.0), (512, 1, 0.5)])
 def test_merged_forward_matches_per_model(cuda, B, K, scale):
-    """rn_field_fwd_merged (chunks of rays, models' tiles interleaved) vs
-    rn_field_fwd: identical per-sample arithmetic, so sigma / rgb and the
-    encoding cache are bit-exact."""
+    """rn_field_fwd_merged (chunks of rays, models' tiles interleaved; encoded
+    in merged order or per tile) vs rn_field_fwd: identical per-sample
+    arithmetic, so sigma / rgb and the encoding cache are bit-exact."""
     esf = 1 / 256 if scale > 0.5 else 0.0
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
     to = lambda a: torch.from_numpy(a).to(cuda)
     outs = []
-    for merged in (True, False):
-        r.merged_fwd = merged
+    # merged kernel with merged-order encoding, with per-tile encoding, per-model kernel
+    for merged, enc in ((True, True), (True, False), (False, False)):
+        r.merged_fwd, r.merged_encode = merged, enc
         ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=esf)
         w = r.ws
         off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
@@ -211,9 +212,10 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd = K <= 4
-    for a, b in zip(*outs):
-        assert torch.equal(a, b)
+    r.merged_fwd, r.merged_encode = K <= 4, True
+    for o2 in outs[1:]:
+        for a, b in zip(outs[0], o2):
+            assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("p,K", [(0.0, 2), (1.0, 3)])

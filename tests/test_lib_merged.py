@@ -16,9 +16,12 @@ def test_merged_entry_points_validate_without_gpu():
     with pytest.raises(RuntimeError, match="rn_bwd_plan: bad sizes"):
         L.bwd_plan(*P[:5], 8, 9, 0, 0, 1024, 512, 10, *P[:6])
     with pytest.raises(RuntimeError, match="n_models <= 4"):
-        L.field_fwd_merged(*P[:8], 8, 5, *P[:11], 256, 512, None)
+        L.field_fwd_merged(*P[:8], 8, 5, *P[:13], 256, 512, None)
     with pytest.raises(RuntimeError, match="threads"):
-        L.field_fwd_merged(*P[:8], 8, 2, *P[:11], 256, 100, None)
+        L.field_fwd_merged(*P[:8], 8, 2, *P[:13], 256, 100, None)
+    V = ctypes.c_void_p(8)      # never dereferenced: the check fails first
+    with pytest.raises(RuntimeError, match="merged-order encoding needs"):
+        L.field_fwd_merged(*[V] * 8, 8, 2, *[V] * 10, None, V, V, 256, 512, None)
     # scratch must hold a chunk plus one ray of every model
     with pytest.raises(RuntimeError, match="scratch_rows must be"):
         L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 2047, None, 1024, 256, *P[:4])
