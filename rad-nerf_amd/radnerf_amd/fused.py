@@ -126,8 +126,10 @@ class FusedMLRenderer:
         self.merged_fwd = model.size <= 4
         # merged forward: encode each chunk in merged (ray, t, model) order
         # first (tiles mixing the sub-NeRFs of a ray stretch share more grid
-        # lines), then the per-model MLP tiles read the encoding cache
-        self.merged_encode = True
+        # lines: 20.9 vs 28.2 per sample, tools/fwd_lines_sim.py), then the
+        # per-model MLP tiles read the encoding cache.  C3: field_fwd 1.095 ->
+        # 1.03 ms.  One sub-NeRF has nothing to interleave.
+        self.merged_encode = model.size > 1
         self.merged_fwd_blocks = 256
         self.merged_fwd_threads = 512
         self.merged_blocks = 256

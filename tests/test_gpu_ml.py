@@ -212,7 +212,7 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd, r.merged_encode = K <= 4, True
+    r.merged_fwd, r.merged_encode = K <= 4, K > 1
     for o2 in outs[1:]:
         for a, b in zip(outs[0], o2):
             assert torch.equal(a, b)
