@@ -1410,7 +1410,7 @@ __global__ void __launch_bounds__(1024)
 k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
     __shared__ LvTab sT;
-    __shared__ int32_t sCh[2 + 2 * FM_KMAX];
+    __shared__ int32_t sCh[2][2 + 2 * FM_KMAX];      // this and the previous chunk
     const int K = m.n_models, B = m.n_rays;
     for (int k = 0; k < K; ++k)
         rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
@@ -1422,7 +1422,40 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     int ticket = 0, n_chunks = 0;
     if (threadIdx.x == 0) { n_chunks = m.queue[1]; ticket = atomicAdd(m.queue + 2, 1); }
-    for (;;) {
+
+    // per-model MLP tile u of chunk descriptor ch (tile i of model 0, tile i
+    // of model 1, ...); false: past the end
+    auto mlp_tile = [&](const int32_t* ch, int u) {
+        const int k = u % K, t = u / K;
+        const int n_k = ch[2 + FM_KMAX + k];
+        if (t * 32 >= n_k) return;                           // wave-uniform
+        rn_lds_order();
+        const int i = t * 32 + c;
+        const bool valid = i < n_k;
+        const int64_t s = ch[2 + k] + (valid ? i : 0);
+        FwdState st;
+        float ux, uy, uz;
+        constexpr int TC = ENC_M ? CACHE_READ_NT : CACHE;
+        tile_forward_s<1, TC>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
+                              valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
+                              st, ux, uy, uz);
+        if (valid && h == 0) {
+            a.sigma[s] = expf(st.g0);
+            a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
+            a.rgb[3 * s + 1] = (float)(rn_half)sigmoidf(st.out[1]);
+            a.rgb[3 * s + 2] = (float)(rn_half)sigmoidf(st.out[2]);
+        }
+    };
+    auto mlp_tiles = [&](const int32_t* ch) {
+        int max_t = 0;
+        for (int k = 0; k < K; ++k) max_t = max(max_t, (ch[2 + FM_KMAX + k] + 31) >> 5);
+        return max_t * K;
+    };
+
+    bool prev_live = false;
+    for (int it = 0;; ++it) {
+        int32_t* cur = sCh[it & 1];
+        const int32_t* prev = sCh[(it & 1) ^ 1];
         __syncthreads();
         if (threadIdx.x == 0) {
             const int ch = ticket;
@@ -1434,60 +1467,48 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
                     d[q] = reinterpret_cast<const int4*>(m.desc + (size_t)ch * CH_DESC)[q];
             }
             const int32_t* di = reinterpret_cast<const int32_t*>(d);
-            sCh[0] = ch < n_chunks ? di[0] : B;
-            sCh[1] = ch < n_chunks ? di[1] : B;
+            cur[0] = ch < n_chunks ? di[0] : B;
+            cur[1] = ch < n_chunks ? di[1] : B;
             for (int k = 0; k < K; ++k) {
-                sCh[2 + k] = di[4 + k];
-                sCh[2 + FM_KMAX + k] = ch < n_chunks ? di[4 + MB_KMAX + k] : 0;
+                cur[2 + k] = di[4 + k];
+                cur[2 + FM_KMAX + k] = ch < n_chunks ? di[4 + MB_KMAX + k] : 0;
             }
         }
         __syncthreads();
-        if (sCh[0] >= B) break;
-        if (ENC_M) {
-            // 1. encode the chunk in merged (ray, t, model) order: a tile mixes
-            // the sub-NeRFs of one ray stretch, so its corners share more lines
-            // (tools/fwd_lines_sim.py: 20.9 vs 28.2 lines per sample); the
-            // encodings go to the cache the MLP tiles and the backward read
-            const int p_base = m.mstart[sCh[0]], n_p = m.mstart[sCh[1]] - p_base;
-            for (int u = wid; u * 32 < n_p; u += waves) {
-                const int q = u * 32 + c;
-                const bool valid = q < n_p;
-                const int64_t s = m.perm[p_base + (valid ? q : 0)];
-                float x, y, z, dx, dy, dz;
-                load_sample<1>(a, s, x, y, z, dx, dy, dz);
-                const float ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
-                const float uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
-                const float uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-                half8 e0, e1;
-                encode_lane(a, sT, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, e0, e1);
-                if (valid) { half8* fc = cache_slot(a, s); fc[0] = e0; fc[1] = e1; }
-            }
-            __syncthreads();
+        const bool live = cur[0] < B;
+        if (!ENC_M) {
+            if (!live) break;
+            const int nt = mlp_tiles(cur);
+            for (int u = wid; u < nt; u += waves) mlp_tile(cur, u);
+            continue;
         }
-        // 2. (or only) the per-model tiles, interleaved across models
-        int max_t = 0;
-        for (int k = 0; k < K; ++k) max_t = max(max_t, (sCh[2 + FM_KMAX + k] + 31) >> 5);
-        for (int u = wid; u < max_t * K; u += waves) {
-            const int k = u % K, t = u / K;
-            const int n_k = sCh[2 + FM_KMAX + k];
-            if (t * 32 >= n_k) continue;                     // wave-uniform
-            rn_lds_order();
-            const int i = t * 32 + c;
-            const bool valid = i < n_k;
-            const int64_t s = sCh[2 + k] + (valid ? i : 0);
-            FwdState st;
-            float ux, uy, uz;
-            constexpr int TC = ENC_M ? CACHE_READ_NT : CACHE;
-            tile_forward_s<1, TC>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
-                                  valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
-                                  st, ux, uy, uz);
-            if (valid && h == 0) {
-                a.sigma[s] = expf(st.g0);
-                a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
-                a.rgb[3 * s + 1] = (float)(rn_half)sigmoidf(st.out[1]);
-                a.rgb[3 * s + 2] = (float)(rn_half)sigmoidf(st.out[2]);
-            }
+        // Merged-order encoding, software-pipelined over chunks: iteration it
+        // encodes chunk it in merged (ray, t, model) order into the encoding
+        // cache -- a tile mixes the sub-NeRFs of one ray stretch, so its
+        // corners share more lines (tools/fwd_lines_sim.py: 20.9 vs 28.2 lines
+        // per sample) -- and runs the per-model MLP tiles of chunk it - 1,
+        // whose encodings the barrier above published; one work list, no
+        // barrier between the two kinds of tile.
+        if (!live && !prev_live) break;
+        int p_base = 0, n_p = 0;
+        if (live) { p_base = m.mstart[cur[0]]; n_p = m.mstart[cur[1]] - p_base; }
+        const int nA = (n_p + 31) >> 5;
+        const int nB = prev_live ? mlp_tiles(prev) : 0;
+        for (int u = wid; u < nA + nB; u += waves) {
+            if (u >= nA) { mlp_tile(prev, u - nA); continue; }
+            const int q = u * 32 + c;
+            const bool valid = q < n_p;
+            const int64_t s = m.perm[p_base + (valid ? q : 0)];
+            float x, y, z, dx, dy, dz;
+            load_sample<1>(a, s, x, y, z, dx, dy, dz);
+            const float ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
+            const float uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
+            const float uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
+            half8 e0, e1;
+            encode_lane(a, sT, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, e0, e1);
+            if (valid) { half8* fc = cache_slot(a, s); fc[0] = e0; fc[1] = e1; }
         }
+        prev_live = live;
     }
 }
 
