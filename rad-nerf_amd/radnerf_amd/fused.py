@@ -131,7 +131,9 @@ class FusedMLRenderer:
         # 1.03 ms.  One sub-NeRF has nothing to interleave.
         self.merged_encode = model.size > 1
         self.merged_fwd_blocks = 256
-        self.merged_fwd_threads = 512
+        # 16 waves: with the merged-order encode, C3 step 5.13 ms vs 5.16 at 8
+        # (tools/step_variants.py, profiles/r01/step_variants_fwd_shape.json)
+        self.merged_fwd_threads = 1024
         self.merged_blocks = 256
         # chunk of merged samples per queue ticket: 1024 keeps a block's staged
         # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
