@@ -120,9 +120,10 @@ class FusedMLRenderer:
         self.merged_bwd = 1 < model.size <= 8      # rn_field_bwd_merged: K <= 8
         # forward evaluating the K models' tiles of a chunk interleaved
         # (rn_field_fwd_merged, K <= 4; bit-exact with rn_field_fwd).  One
-        # 8-wave block per CU keeps a chunk's rays in that CU's L1, so the second
+        # block per CU keeps a chunk's rays in that CU's L1, so the second
         # model's corners hit lines the first fetched: C3 1.12 ms vs 1.30 ms
-        # (tools/fwd_blocks_sweep.py; 2 blocks per CU 1.17, 3 x 4 waves 1.35)
+        # before the merged-order encode (tools/fwd_blocks_sweep.py; 2 blocks
+        # per CU 1.17, 3 x 4 waves 1.35)
         self.merged_fwd = model.size <= 4
         # merged forward: encode each chunk in merged (ray, t, model) order
         # first (tiles mixing the sub-NeRFs of a ray stretch share more grid
