@@ -152,8 +152,22 @@ __device__ int march_ray_wave(float ox, float oy, float oz, float dx, float dy, 
         float t = tb;
         if (c.esf == 0.0f) {            // constant dt (scale <= 0.5 scenes): same adds, no clamp
             const float d0 = rn_calc_dt(0.0f, c.esf, c.max_samples, c.grid_size, c.dt_scale);
+            // Inside one binade [2^e, 2^(e+1)) every t is a multiple of its ulp
+            // u and fl(t + d0) = t + r with r = round_u(d0) the same for every
+            // t (round-to-nearest is translation invariant on that grid; with
+            // a tie, only the first step can differ, which the second-step
+            // comparison rejects).  So t_j = tb + j r exactly, one fma per
+            // lane, whenever the chunk stays inside tb's binade; otherwise
+            // the serial adds below.
+            const float s1 = tb + d0, r = s1 - tb, s2 = s1 + d0;
+            const float bend = __uint_as_float((__float_as_uint(tb) & 0x7f800000u) + 0x00800000u);
+            const float tj = fmaf((float)lane, r, tb);
+            if (s2 - s1 == r && tb > 0.0f && __builtin_amdgcn_ballot_w64(!(tj < bend)) == 0) {
+                t = tj;
+            } else {
 #pragma unroll 16
-            for (int i = 0; i < RN_WAVE - 1; ++i) { const float nt = t + d0; t = i < lane ? nt : t; }
+                for (int i = 0; i < RN_WAVE - 1; ++i) { const float nt = t + d0; t = i < lane ? nt : t; }
+            }
         } else {
 #pragma unroll 8
             for (int i = 0; i < RN_WAVE - 1; ++i) {
