@@ -60,6 +60,13 @@ struct CompactSink {
     }
 };
 
+// 1 / mip_bound with mip_bound = fminf(2^(mip-1), scale) (raymarching.cu:
+// 213-214), bit-exact without a per-query division: the reciprocal of a power
+// of two is exact, and 1 / scale is loop-invariant
+__device__ __forceinline__ float mip_bound_inv(int mip, float scale) {
+    return scalbnf(1.0f, mip - 1) < scale ? scalbnf(1.0f, 1 - mip) : 1.0f / scale;
+}
+
 // One occupancy query + step of raymarching.cu:205-233.  Returns true if the
 // cell at t is occupied; otherwise advances t past the cell exit.
 __device__ __forceinline__ bool march_step(float& t, float ox, float oy, float oz,
@@ -75,7 +82,7 @@ __device__ __forceinline__ bool march_step(float& t, float ox, float oy, float o
     const int mip = max(rn_mip_from_pos(x, y, z, c.cascades),
                         rn_mip_from_dt(dt, c.grid_size, c.cascades));
     const float mb = fminf(scalbnf(1.0f, mip - 1), c.scale);
-    const float mbi = 1 / mb;
+    const float mbi = mip_bound_inv(mip, c.scale);
     const float gm1 = c.grid_size - 1.0f;
     const int nx = (int)rn_clampf(0.5f * fmaf(x, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
     const int ny = (int)rn_clampf(0.5f * fmaf(y, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
@@ -108,7 +115,7 @@ __device__ __forceinline__ bool march_query(float t, float ox, float oy, float o
     const int mip = max(rn_mip_from_pos(x, y, z, c.cascades),
                         rn_mip_from_dt(dt, c.grid_size, c.cascades));
     const float mb = fminf(scalbnf(1.0f, mip - 1), c.scale);
-    const float mbi = 1 / mb;
+    const float mbi = mip_bound_inv(mip, c.scale);
     const float gm1 = c.grid_size - 1.0f;
     const int nx = (int)rn_clampf(0.5f * fmaf(x, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
     const int ny = (int)rn_clampf(0.5f * fmaf(y, mbi, 1.0f) * c.grid_size, 0.0f, gm1);
@@ -189,16 +196,22 @@ __device__ int march_ray_wave(float ox, float oy, float oz, float dx, float dy, 
         int cur = cand ? __builtin_ctzll(cand) : RN_WAVE;
         int emitted = 0;
         bool full = false;
+        const bool capfree = n + RN_WAVE < cap;          // this chunk cannot reach the cap
         while (cur < RN_WAVE) {
             const uint64_t from = ~0ull << cur;
             if ((occ_m >> cur) & 1ull) {
                 const uint64_t stop = ~occ_m & from;
-                int end = stop ? __builtin_ctzll(stop) : RN_WAVE;
-                if (n + emitted + (end - cur) >= cap) { end = cur + (cap - n - emitted); full = true; }
-                mark |= from & (end < RN_WAVE ? ~(~0ull << end) : ~0ull);
-                emitted += end - cur;
+                const int end = stop ? __builtin_ctzll(stop) : RN_WAVE;
                 need = -INFINITY;
-                if (full) break;
+                if (!capfree && n + emitted + (end - cur) >= cap) {
+                    const int e2 = cur + (cap - n - emitted);
+                    mark |= from & (e2 < RN_WAVE ? ~(~0ull << e2) : ~0ull);
+                    emitted += e2 - cur;
+                    full = true;
+                    break;
+                }
+                mark |= from & ((stop & (0ull - stop)) - 1ull);   // steps [cur, end)
+                emitted += end - cur;
                 cur = (end < RN_WAVE && ((alive_m >> end) & 1ull)) ? end : RN_WAVE;
             } else {
                 mark |= 1ull << cur;
