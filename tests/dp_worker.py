@@ -1,0 +1,76 @@
+"""GPU worker of tests/test_gpu_dist.py (not a test module): one rank of the
+ray-batch data-parallel step (radnerf_amd/dist.py, bench.py --gpus N)
+rehearsed on ONE GPU over gloo.  Rank r renders its own rays; the flat
+gradient is averaged over the ranks.  Rank 0 also renders every rank's rays
+in one process, averages those gradients and writes the comparison to the
+JSON path in argv[1]."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "rad-nerf_amd")]
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from radnerf_amd import dist as rdist  # noqa: E402
+from radnerf_amd import synthetic as S  # noqa: E402
+from radnerf_amd.fused import FusedMLRenderer  # noqa: E402
+from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
+
+
+def rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def inputs(rank, B, K, scale, dev):
+    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B, scale, seed=1000 * rank))
+    nz = torch.from_numpy(S.noise(K, B, seed=2 + 7919 * rank)).to(dev)
+    sd = [torch.from_numpy(s).to(dev) for s in S.loss_seeds(B, K, seed=4 + rank)]
+    return o, d, nz, sd
+
+
+def step(r, o, d, nz, sd, bg, views):
+    _, _, _, g_out, _ = r.forward(o, d, d, nz, bg, 1e-4, 0.0)
+    r.backward(o, d, d, g_out, bg, *sd, None, 1e-4, grid_grad=views[0], mlp_grad=views[1],
+               gate_grad=views[2])
+
+
+def main(out_path):
+    rank, _, world = rdist.init(backend="gloo")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    B, K, scale = 1024, 2, 0.5
+    model = MNGP(scale, size=K, seed=3).to(dev)
+    gate = Ray_Gate(K, seed=4).to(dev)
+    bits = S.bitfields(K, model.cascades, p=0.5, seed=1)
+    with torch.no_grad():
+        for i in range(K):
+            getattr(model, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    bg = torch.ones(3, device=dev)
+    params = [model.xyz_encoder.params, model.mlp_params, gate.params]
+    r = FusedMLRenderer(model, gate, B)
+    ar = rdist.GradAllReduce(params, dev)
+    ar.zero()
+    o, d, nz, sd = inputs(rank, B, K, scale, dev)
+    step(r, o, d, nz, sd, bg, ar.views)
+    ar.reduce()
+    torch.cuda.synchronize()
+    if rank == 0:
+        ref = rdist.GradAllReduce(params, dev)      # not reduced: a local buffer
+        ref.zero()
+        for q in range(world):
+            step(r, *inputs(q, B, K, scale, dev), bg, ref.views)
+        ref.flat.div_(world)
+        torch.cuda.synchronize()
+        res = {"world": world, "grid_rel": rel(ar.views[0], ref.views[0]),
+               "mlp_rel": rel(ar.views[1], ref.views[1]),
+               "gate_rel": rel(ar.views[2], ref.views[2])}
+        with open(out_path, "w") as f:
+            json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
