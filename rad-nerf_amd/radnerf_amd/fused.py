@@ -230,7 +230,7 @@ class FusedMLRenderer:
                           w.depth_k.data_ptr(), w.rgb_k.data_ptr(), w.ws.data_ptr(), st)
         # per-ray outputs of all G gated sub-NeRFs (here: the K rendered ones;
         # pinned.PinnedMLRenderer gathers them from every rank)
-        ok, dk, rk = self._all_model_outputs()
+        ok, dk, rk = self._gather_model_outputs()
         rgb = torch.empty(B, 3, device=rays_o.device)
         opacity = torch.empty(B, device=rays_o.device)
         depth = torch.empty(B, G, device=rays_o.device)
@@ -242,8 +242,13 @@ class FusedMLRenderer:
                         opacity.data_ptr(), depth.data_ptr(), st)
         return rgb, opacity, depth, out_gate, imp
 
-    def _all_model_outputs(self):
-        """(opacity, depth, rgb) per (sub-NeRF, ray) of every gated sub-NeRF."""
+    def _gather_model_outputs(self):
+        """(opacity, depth, rgb) per (sub-NeRF, ray) of every gated sub-NeRF,
+        after this step's composite (forward)."""
+        return self._model_outputs()
+
+    def _model_outputs(self):
+        """The same, as the forward left them (backward)."""
         w = self.ws
         return w.opacity_k, w.depth_k, w.rgb_k
 
@@ -336,7 +341,7 @@ class FusedMLRenderer:
         grid_grad = torch.zeros_like(m.xyz_encoder.params) if grid_grad is None else grid_grad
         mlp_grad = torch.zeros_like(m.mlp_params) if mlp_grad is None else mlp_grad
         gate_grad = torch.zeros_like(g.params) if gate_grad is None else gate_grad
-        ok, _, rk = self._all_model_outputs()
+        ok, _, rk = self._model_outputs()
         dgate = self._dgate(B, G)
         self._ev("combine_bw", L.ml_combine_bw, dL_drgb.data_ptr(), dL_dopacity.data_ptr(),
                  ok.data_ptr(), rk.data_ptr(), bg.data_ptr(), B, G, dgate.data_ptr(), st)

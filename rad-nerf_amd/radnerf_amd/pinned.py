@@ -94,7 +94,12 @@ class PinnedMLRenderer(FusedMLRenderer):
         return super().forward(rays_o, rays_d, gate_in2, noise[self.k0:self.k1], bg, T_threshold,
                                exp_step_factor)
 
-    def _all_model_outputs(self):
+    def _model_outputs(self):
+        if self.world == 1:
+            return super()._model_outputs()
+        return self.opacity_all, self.depth_all, self.rgb_all
+
+    def _gather_model_outputs(self):
         w, B = self.ws, self.ws.B
         if self.world == 1:
             return w.opacity_k, w.depth_k, w.rgb_k

@@ -62,14 +62,15 @@ def _worker(rank, world, port, q):
         r.ws.opacity_k.copy_(kk * 100 + bb)
         r.ws.depth_k.copy_(-(kk * 100 + bb))
         r.ws.rgb_k.copy_((kk * 100 + bb)[..., None] + torch.tensor([0.1, 0.2, 0.3]))
-        op, dp, rgb = r._all_model_outputs()
+        op, dp, rgb = r._gather_model_outputs()
+        ok_cached = all(a is b for a, b in zip((op, dp, rgb), r._model_outputs()))
         KA = torch.arange(K, dtype=torch.float32)[:, None]
         ok_gather = (torch.equal(op, KA * 100 + bb) and torch.equal(dp, -(KA * 100 + bb))
                      and torch.allclose(rgb, (KA * 100 + bb)[..., None]
                                         + torch.tensor([0.1, 0.2, 0.3])))
         # (B, K) per-ray tensors: this rank's columns
         gate = torch.arange(B * K, dtype=torch.float32).view(B, K)
-        ok_cols = torch.equal(r._local_cols(gate), gate[:, k0:k1])
+        ok_cols = torch.equal(r._local_cols(gate), gate[:, k0:k1]) and ok_cached
         # gradient sum: grid partials add, MLP rows only on their owner, gate on rank 0
         ar = rdist.GradAllReduce([m.xyz_encoder.params, m.mlp_params, g.params], "cpu")
         ar.views[0].fill_(1.0)
