@@ -218,6 +218,35 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
             assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("mc,blocks,threads", [(64, 3, 256), (300, 37, 1024), (4096, 256, 512)])
+def test_merged_forward_chunking(cuda, mc, blocks, threads):
+    """The merged forward's pipeline (merged-order encode of chunk i beside the
+    MLP tiles of chunk i - 1) over many small chunks per block, ragged chunks
+    and few blocks: still bit-exact with the per-model kernel."""
+    B, K = 2048, 3
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
+    r = get_renderer(m, g, B)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    outs = []
+    for merged in (True, False):
+        r.merged_fwd, r.merged_encode = merged, merged
+        r.max_chunk, r.merged_fwd_blocks, r.merged_fwd_threads = mc, blocks, threads
+        ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
+        w = r.ws
+        n = int(w.meta[0])
+        outs.append((w.sigma[:n].clone(), w.rgb[:n].clone()))
+    r.merged_fwd, r.merged_encode, r.max_chunk = True, True, 1024
+    r.merged_fwd_blocks, r.merged_fwd_threads = 256, 1024
+    # padding slots between segments are never written: compare the samples
+    w = r.ws
+    off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
+    idx = np.concatenate([np.arange(off[k, rr], off[k, rr] + cnt[k, rr])
+                          for k in range(K) for rr in range(B)]).astype(np.int64)
+    ii = torch.from_numpy(idx).to(cuda)
+    for a, b in zip(*outs):
+        assert torch.equal(a[ii], b[ii])
+
+
 @pytest.mark.parametrize("p,K", [(0.0, 2), (1.0, 3)])
 def test_merged_backward_edge_occupancy(cuda, p, K):
     """Empty grid (no samples at all: zero chunks) and a full grid with K = 3
