@@ -299,8 +299,10 @@ __global__ void __launch_bounds__(1024)
 k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ counts,
                 int32_t* __restrict__ offsets, int32_t* __restrict__ seg_base,
                 int32_t* __restrict__ seg_count, int32_t* __restrict__ meta) {
+    // SCAN_PT consecutive elements per thread per pass: one wave scan and one
+    // cross-wave scan per SCAN_PT * blockDim elements (a latency-bound chain)
+    constexpr int SCAN_PT = 4;
     __shared__ int wsum[16];
-    __shared__ int carry_s;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nthr = blockDim.x, nw = nthr >> 6;
     int base = 0, total = 0;
@@ -308,10 +310,15 @@ k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ cou
         const int32_t* cin = counts + (size_t)k * n_per;
         int32_t* cout = offsets + (size_t)k * n_per;
         int carry = 0;
-        for (int c0 = 0; c0 < n_per; c0 += nthr) {
-            const int i = c0 + tid;
-            const int v = i < n_per ? cin[i] : 0;
-            const int incl = rn_wave_incl_sum_i(v);
+        for (int c0 = 0; c0 < n_per; c0 += nthr * SCAN_PT) {
+            const int i0 = c0 + tid * SCAN_PT;
+            int v[SCAN_PT], loc = 0;
+#pragma unroll
+            for (int j = 0; j < SCAN_PT; ++j) {
+                v[j] = i0 + j < n_per ? cin[i0 + j] : 0;
+                loc += v[j];
+            }
+            const int incl = rn_wave_incl_sum_i(loc);
             if (lane == 63) wsum[wid] = incl;
             __syncthreads();
             if (wid == 0) {
@@ -320,8 +327,12 @@ k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ cou
                 if (lane < nw) wsum[lane] = s;
             }
             __syncthreads();
-            const int wpre = wid > 0 ? wsum[wid - 1] : 0;
-            if (i < n_per) cout[i] = base + carry + wpre + incl - v;
+            int run = base + carry + (wid > 0 ? wsum[wid - 1] : 0) + incl - loc;
+#pragma unroll
+            for (int j = 0; j < SCAN_PT; ++j) {
+                if (i0 + j < n_per) cout[i0 + j] = run;
+                run += v[j];
+            }
             const int chunk_total = wsum[nw - 1];
             __syncthreads();
             carry += chunk_total;
@@ -331,7 +342,6 @@ k_scan_segments(int n_seg, int n_per, int align, const int32_t* __restrict__ cou
         base = ((base + carry + align - 1) / align) * align;
     }
     if (tid == 0) { meta[0] = base; meta[1] = total; }
-    (void)carry_s;
 }
 
 // ----------------------------------------------------------------------------
