@@ -1597,6 +1597,32 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
+    if (K == 2 && staged) {
+        // merge path: lane j emits merged positions [j L, (j+1) L); it finds
+        // how many of them come from model 0 by a binary search on its
+        // diagonal (model 0 first on equal t, as below), then merges serially
+        // -- ~log2(n) + L dependent LDS reads per lane instead of a search
+        // per sample (C3: 0.064 -> 0.040 ms with k_bwd_chunks)
+        const float* A = st + loc[0];
+        const float* Bv = st + loc[1];
+        const int nA = cnt[0], nB = cnt[1], n = nA + nB;
+        const int L = (n + RN_WAVE - 1) / RN_WAVE;
+        const int d = min(lane * L, n);
+        int lo = max(0, d - nB), hi = min(d, nA);
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (A[mid] <= Bv[d - 1 - mid]) lo = mid + 1; else hi = mid;
+        }
+        int a = lo, b = d - lo;
+        const int e = min(d + L, n);
+        for (int q = d; q < e; ++q) {
+            const bool takeA = a < nA && (b >= nB || A[a] <= Bv[b]);
+            perm[ms + q] = takeA ? off[0] + a : off[1] + b;
+            a += takeA ? 1 : 0;
+            b += takeA ? 0 : 1;
+        }
+        return;
+    }
     for (int k = 0; k < K; ++k) {
         for (int i = lane; i < cnt[k]; i += RN_WAVE) {
             const float t = staged ? st[loc[k] + i] : ts[off[k] + i];
