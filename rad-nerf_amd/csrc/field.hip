@@ -200,31 +200,60 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
     const bool load = valid && !(a.dbg & 128);
 #pragma unroll
     for (int lb = 0; lb < RN_L; lb += 4) {
-        LevelPos P[4];
+        // per level: the cell's x, the weights' fractions, and the x-free part
+        // of tcnn grid_index for the 4 (y, z) rows: dense levels
+        // y res + z res^2 (+ res / res^2; u24 exact, res <= 128), hashed
+        // y P1 ^ z P2 with (y+1) P1 = y P1 + P1.  Both wave halves need them
+        // for the same sample, so each half computes one level of a pair and
+        // v_permlane32_swap hands it to the other (lanes 0-31: level lb + up,
+        // lanes 32-63: lb + up + 1).
+        uint32_t GX[4], ROW[4][4];
+        float FX[4], FY[4], FZ[4];
+#pragma unroll
+        for (int up = 0; up < 4; up += 2) {
+            const LvConst lm = lv_const(T, a.gm, lb + up + h);
+            const LevelPos p = level_pos(lm.sc, ux, uy, uz);
+            uint32_t rw[4];
+            if (lm.dense) {
+                const uint32_t b = __umul24(p.gy, lm.res) + __umul24(p.gz, lm.res2);
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    rw[r] = b + ((r & 1) ? lm.res : 0u) + ((r >> 1) ? lm.res2 : 0u);
+            } else {
+                const uint32_t y0 = p.gy * 2654435761u, z0 = p.gz * 805459861u;
+                const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) rw[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
+            }
+            auto xch = [&](uint32_t v, uint32_t& lo, uint32_t& hi) {
+                const auto r2 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+                lo = r2[0]; hi = r2[1];
+            };
+            uint32_t t0, t1;
+            xch(p.gx, GX[up], GX[up + 1]);
+            xch(__float_as_uint(p.fx), t0, t1); FX[up] = __uint_as_float(t0); FX[up + 1] = __uint_as_float(t1);
+            xch(__float_as_uint(p.fy), t0, t1); FY[up] = __uint_as_float(t0); FY[up + 1] = __uint_as_float(t1);
+            xch(__float_as_uint(p.fz), t0, t1); FZ[up] = __uint_as_float(t0); FZ[up + 1] = __uint_as_float(t1);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) xch(rw[r], ROW[up][r], ROW[up + 1][r]);
+        }
         uint32_t off[16];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
+            // the lane's 4 corners of level lb + u: x = gx + h on the 4 rows.
+            // The level is wave-uniform here, so only one branch runs.
             const LvConst lc = lv_const(T, a.gm, lb + u);
-            P[u] = level_pos(lc.sc, ux, uy, uz);
-            // tcnn grid_index of the lane's 4 corners (x = gx + h, rows (dy, dz)),
-            // the row part shared: dense levels x + y res + z res^2 (u24 exact,
-            // res <= 128), hashed x ^ y P1 ^ z P2 with (y+1) P1 = y P1 + P1.
-            // The level is wave-uniform, so only one branch runs.
-            const uint32_t x = P[u].gx + (uint32_t)h;
+            const uint32_t x = GX[u] + (uint32_t)h;
             uint32_t idx[4];
             if (lc.dense) {
-                const uint32_t b = x + __umul24(P[u].gy, lc.res) + __umul24(P[u].gz, lc.res2);
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const uint32_t d = b + ((r & 1) ? lc.res : 0u) + ((r >> 1) ? lc.res2 : 0u);
-                    idx[r] = d >= lc.hs ? d - lc.hs : d;
+                    const uint32_t d = x + ROW[u][r];
+                    idx[r] = min(d, d - lc.hs);      // d >= hs ? d - hs : d  (d < 2 hs)
                 }
             } else {
-                const uint32_t y0 = P[u].gy * 2654435761u, z0 = P[u].gz * 805459861u;
-                const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
 #pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    idx[r] = (x ^ ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0)) & (lc.hs - 1u);
+                for (int r = 0; r < 4; ++r) idx[r] = (x ^ ROW[u][r]) & (lc.hs - 1u);
             }
             // one v_add_lshl per corner; invalid lanes start past num_records
             // (the table is < 2^31 B)
@@ -239,12 +268,12 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
         for (int u = 0; u < 4; ++u) {
             float a0 = 0.f, a1 = 0.f;
             // corner weight (wx * wy) * wz, tcnn's dimension order
-            const float wx = h ? P[u].fx : 1.0f - P[u].fx;
-            const float wy0 = 1.0f - P[u].fy, wz0 = 1.0f - P[u].fz;
-            const float wxy0 = wx * wy0, wxy1 = wx * P[u].fy;
+            const float wx = h ? FX[u] : 1.0f - FX[u];
+            const float wy0 = 1.0f - FY[u], wz0 = 1.0f - FZ[u];
+            const float wxy0 = wx * wy0, wxy1 = wx * FY[u];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float w = ((r & 1) ? wxy1 : wxy0) * ((r >> 1) ? P[u].fz : wz0);
+                const float w = ((r & 1) ? wxy1 : wxy0) * ((r >> 1) ? FZ[u] : wz0);
                 const uint32_t v = raw[4 * u + r];
                 a0 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu)), a0);
                 a1 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v >> 16)), a1);
