@@ -42,8 +42,7 @@ __device__ SegOut seg_forward(const float* __restrict__ sig, const float* __rest
         const float om = 1.0f - a;
         // transmittance after this sample = T * prod_{j<=i} (1-a_j)
         const float pin = rn_wave_incl_prod(lane == 0 ? T * om : om);
-        float pex = __shfl_up(pin, 1);
-        if (lane == 0) pex = T;
+        const float pex = rn_wave_shr1(pin, T);
         const float w = a * pex;
         const unsigned long long stop = __ballot(valid && pin <= thr);
         int last = RN_WAVE - 1;
@@ -58,7 +57,7 @@ __device__ SegOut seg_forward(const float* __restrict__ sig, const float* __rest
             aR = fmaf(w, c0, aR); aG = fmaf(w, c1, aG); aB = fmaf(w, c2, aB);
             aD = fmaf(w, t, aD); aO += w;
         }
-        T = __shfl(pin, RN_WAVE - 1);
+        T = rn_wave_last(pin);
     }
     SegOut o;
     o.O = rn_wave_sum(aO); o.D = rn_wave_sum(aD);
@@ -104,8 +103,7 @@ __device__ void seg_backward(const float* __restrict__ sig, const float* __restr
         }
         const float om = 1.0f - a;
         const float pin = rn_wave_incl_prod(lane == 0 ? T * om : om);
-        float pex = __shfl_up(pin, 1);
-        if (lane == 0) pex = T;
+        const float pex = rn_wave_shr1(pin, T);
         const float w = a * pex;
         const unsigned long long stop = __ballot(valid && pin <= thr);
         const int last = stop ? __ffsll((long long)stop) - 1 : RN_WAVE - 1;
@@ -130,10 +128,10 @@ __device__ void seg_backward(const float* __restrict__ sig, const float* __restr
             dsig[s] = 0.f; drgb[3 * s] = 0.f; drgb[3 * s + 1] = 0.f; drgb[3 * s + 2] = 0.f;
         }
         if (stop) done = true;
-        T = __shfl(pin, RN_WAVE - 1);
-        pr = __shfl(sr, RN_WAVE - 1); pg = __shfl(sg, RN_WAVE - 1);
-        pb = __shfl(sb, RN_WAVE - 1); pd = __shfl(sd, RN_WAVE - 1);
-        pw = __shfl(sw, RN_WAVE - 1);
+        T = rn_wave_last(pin);
+        pr = rn_wave_last(sr); pg = rn_wave_last(sg);
+        pb = rn_wave_last(sb); pd = rn_wave_last(sd);
+        pw = rn_wave_last(sw);
     }
 }
 
@@ -318,15 +316,14 @@ k_distortion_fw(int n_rows, const float* __restrict__ ws, const float* __restric
         const float wt = w * t;
         const float sw = pw + rn_wave_incl_sum(w);
         const float swt = pwt + rn_wave_incl_sum(wt);
-        float ex_w = __shfl_up(sw, 1), ex_wt = __shfl_up(swt, 1);   // exclusive scans
-        if (lane == 0) { ex_w = pw; ex_wt = pwt; }
+        const float ex_w = rn_wave_shr1(sw, pw), ex_wt = rn_wave_shr1(swt, pwt);   // exclusive scans
         if (valid) {
             ws_incl[start + i] = sw;
             wts_incl[start + i] = swt;
             acc += 2.0f * (swt * ex_w - sw * ex_wt) + (1.0f / 3) * w * w * d;
         }
-        pw = __shfl(sw, RN_WAVE - 1);
-        pwt = __shfl(swt, RN_WAVE - 1);
+        pw = rn_wave_last(sw);
+        pwt = rn_wave_last(swt);
     }
     acc = rn_wave_sum(acc);
     if (lane == 0) loss[ray] = acc;

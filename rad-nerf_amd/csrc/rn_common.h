@@ -8,6 +8,7 @@
 // makes per-ray sample counts and sample positions bit-exact between the two.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 #include "radnerf.h"   // the C ABI: definitions below must match these declarations
 
@@ -107,34 +108,67 @@ __device__ __forceinline__ float rn_wave_sum(float v) {
     return v;
 }
 
+// DPP move of v with control CTRL (row_shr:n = 0x110 + n, wave_shr:1 = 0x138):
+// lanes whose source lane is outside the row / wave get `ident`
+template <int CTRL>
+__device__ __forceinline__ float rn_dpp(float ident, float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(ident), __float_as_int(v),
+                                                      CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int rn_dpp_i(int ident, int v) {
+    return __builtin_amdgcn_update_dpp(ident, v, CTRL, 0xf, 0xf, false);
+}
+
+// Inclusive wave64 scan: Hillis-Steele inside each 16-lane row with DPP
+// row shifts (no LDS crossbar), then the row totals (lanes 15, 31, 47) are
+// carried in.  `op` must be commutative (+, *).
+template <typename T, typename Op, typename Dpp>
+__device__ __forceinline__ T rn_wave_incl_scan(T v, T ident, Op op, Dpp dpp) {
+    v = op(v, dpp(ident, v, std::integral_constant<int, 0x111>{}));
+    v = op(v, dpp(ident, v, std::integral_constant<int, 0x112>{}));
+    v = op(v, dpp(ident, v, std::integral_constant<int, 0x114>{}));
+    v = op(v, dpp(ident, v, std::integral_constant<int, 0x118>{}));
+    const int row = rn_lane() >> 4;
+    const T r0 = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 15));
+    const T r1 = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 31));
+    const T r2 = __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 47));
+    const T c01 = op(r0, r1);
+    const T carry = row == 1 ? r0 : (row == 2 ? c01 : op(c01, r2));
+    return row == 0 ? v : op(carry, v);
+}
+
+struct RnDppF {
+    template <int C>
+    __device__ float operator()(float id, float v, std::integral_constant<int, C>) const {
+        return rn_dpp<C>(id, v);
+    }
+};
+struct RnDppI {
+    template <int C>
+    __device__ int operator()(int id, int v, std::integral_constant<int, C>) const {
+        return rn_dpp_i<C>(id, v);
+    }
+};
+
 // inclusive prefix sum across the 64 lanes of a wave
 __device__ __forceinline__ float rn_wave_incl_sum(float v) {
-    const int lane = rn_lane();
-#pragma unroll
-    for (int off = 1; off < RN_WAVE; off <<= 1) {
-        float o = __shfl_up(v, off);
-        if (lane >= off) v += o;
-    }
-    return v;
+    return rn_wave_incl_scan(v, 0.0f, [](float a, float b) { return a + b; }, RnDppF{});
 }
 
 // inclusive prefix product across the 64 lanes of a wave
 __device__ __forceinline__ float rn_wave_incl_prod(float v) {
-    const int lane = rn_lane();
-#pragma unroll
-    for (int off = 1; off < RN_WAVE; off <<= 1) {
-        float o = __shfl_up(v, off);
-        if (lane >= off) v *= o;
-    }
-    return v;
+    return rn_wave_incl_scan(v, 1.0f, [](float a, float b) { return a * b; }, RnDppF{});
+}
+
+// v of lane l - 1 (lane 0: first)
+__device__ __forceinline__ float rn_wave_shr1(float v, float first) { return rn_dpp<0x138>(first, v); }
+
+// v of lane 63, in every lane
+__device__ __forceinline__ float rn_wave_last(float v) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), RN_WAVE - 1));
 }
 
 __device__ __forceinline__ int rn_wave_incl_sum_i(int v) {
-    const int lane = rn_lane();
-#pragma unroll
-    for (int off = 1; off < RN_WAVE; off <<= 1) {
-        int o = __shfl_up(v, off);
-        if (lane >= off) v += o;
-    }
-    return v;
+    return rn_wave_incl_scan(v, 0, [](int a, int b) { return a + b; }, RnDppI{});
 }
