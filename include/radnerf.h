@@ -236,7 +236,7 @@ int rn_seed_scale(const int32_t* seg_base, const int32_t* seg_count, int32_t n_m
 int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const float* scale,
                     float* grid_grad, void* stream);
 
-/* Merged forward (fused training path, n_models <= 4): same outputs as
+/* Merged forward (fused training path, n_models <= 8): same outputs as
  * rn_field_fwd in compact mode, but blocks take rn_bwd_plan's chunks (queue
  * [2] is the forward's ticket) and evaluate the models' tiles of a chunk
  * interleaved, so the K sub-NeRFs' samples of one ray share cached grid

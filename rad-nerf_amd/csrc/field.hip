@@ -1428,23 +1428,27 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
 // K models' tiles of a chunk interleaved (tile i of model 0, tile i of model
 // 1, ...), so the models' samples of the same rays are gathered close in time
 // by the same CU: the second model's corners hit L1/L2 lines the first one
-// fetched (the fine levels otherwise miss L2 for every sample).  All K
-// models' forward fragments sit in LDS (dynamic, K x 24 KB; K <= 4).
+// fetched (the fine levels otherwise miss L2 for every sample).  With
+// K <= FM_LDS_K the K models' forward fragments sit in LDS (dynamic, K x
+// 24 KB); with more (GW), the MLP tiles read them from global memory (L2).
 // Same outputs as k_field_fwd (per-sample arithmetic is identical).
 // ---------------------------------------------------------------------------
-#define FM_KMAX 4
+#define FM_KMAX 8
+#define FM_LDS_K 4
 
-template <int CACHE, bool ENC_M>
+template <int CACHE, bool ENC_M, bool GW>
 __global__ void __launch_bounds__(1024)
 k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
     __shared__ LvTab sT;
     __shared__ int32_t sCh[2][2 + 2 * FM_KMAX];      // this and the previous chunk
     const int K = m.n_models, B = m.n_rays;
-    for (int k = 0; k < K; ++k)
-        rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
-                        a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
-                        FIELD_FWD_FRAGS * RN_FRAG_BYTES);
+    if (!GW) {
+        for (int k = 0; k < K; ++k)
+            rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
+                            a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
+                            FIELD_FWD_FRAGS * RN_FRAG_BYTES);
+    }
     lv_stage(sT, a.gm);
     const int waves = blockDim.x / RN_WAVE;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
@@ -1465,8 +1469,9 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
         FwdState st;
         float ux, uy, uz;
         constexpr int TC = ENC_M ? CACHE_READ_NT : CACHE;
-        tile_forward_s<1, TC>(a, sT, sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS, s,
-                              valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
+        const rn_half* W = GW ? a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS
+                              : sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS;
+        tile_forward_s<1, TC>(a, sT, W, s, valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
                               st, ux, uy, uz);
         if (valid && h == 0) {
             a.sigma[s] = expf(st.g0);
@@ -1969,7 +1974,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
                         const int32_t* perm, int32_t blocks, int32_t threads, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && blocks >= 1,
-                 "bad sizes (n_models <= 4)");
+                 "bad sizes (n_models <= 8)");
     RN_CHECK_ARG(threads >= 64 && threads <= 1024 && threads % 64 == 0, "threads: 64..1024, waves");
     RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count &&
                  chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
@@ -1987,15 +1992,22 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     m.desc = chunk_desc; m.queue = queue;
     m.mstart = mstart; m.perm = perm;
     m.n_rays = (int)n_rays; m.n_models = n_models;
-    const size_t lds = (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
+    const bool gw = n_models > FM_LDS_K;
+    const size_t lds = gw ? 0 : (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(queue + 2, 0, sizeof(int32_t), st) != hipSuccess) {
         rn_set_error("%s: ticket reset failed", __func__);
         return 2;
     }
-    if (mstart) k_field_fwd_merged<CACHE_WRITE, true><<<blocks, threads, lds, st>>>(a, m);
-    else if (feat_cache) k_field_fwd_merged<CACHE_WRITE, false><<<blocks, threads, lds, st>>>(a, m);
-    else k_field_fwd_merged<CACHE_NONE, false><<<blocks, threads, lds, st>>>(a, m);
+#define RN_FM_LAUNCH(C, E)                                                                     \
+    do {                                                                                       \
+        if (gw) k_field_fwd_merged<C, E, true><<<blocks, threads, 0, st>>>(a, m);              \
+        else k_field_fwd_merged<C, E, false><<<blocks, threads, lds, st>>>(a, m);              \
+    } while (0)
+    if (mstart) RN_FM_LAUNCH(CACHE_WRITE, true);
+    else if (feat_cache) RN_FM_LAUNCH(CACHE_WRITE, false);
+    else RN_FM_LAUNCH(CACHE_NONE, false);
+#undef RN_FM_LAUNCH
     RN_CHECK_LAUNCH();
     return 0;
 }

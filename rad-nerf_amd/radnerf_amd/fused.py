@@ -119,12 +119,13 @@ class FusedMLRenderer:
         # (K = 1 has nothing to merge: the per-model kernel is 3 % faster there)
         self.merged_bwd = 1 < model.size <= 8      # rn_field_bwd_merged: K <= 8
         # forward evaluating the K models' tiles of a chunk interleaved
-        # (rn_field_fwd_merged, K <= 4; bit-exact with rn_field_fwd).  One
+        # (rn_field_fwd_merged, K <= 8; bit-exact with rn_field_fwd).  One
         # block per CU keeps a chunk's rays in that CU's L1, so the second
         # model's corners hit lines the first fetched: C3 1.12 ms vs 1.30 ms
         # before the merged-order encode (tools/fwd_blocks_sweep.py; 2 blocks
         # per CU 1.17, 3 x 4 waves 1.35)
-        self.merged_fwd = model.size <= 4
+        # (K > 4: the MLP fragments are read from global memory instead of LDS)
+        self.merged_fwd = model.size <= 8
         # merged forward: encode each chunk in merged (ray, t, model) order
         # first (tiles mixing the sub-NeRFs of a ray stretch share more grid
         # lines: 20.9 vs 28.2 per sample, tools/fwd_lines_sim.py), then the

@@ -189,7 +189,8 @@ def test_merged_backward_chunking(cuda):
             assert rel <= 1e-5, rel
 
 
-@pytest.mark.parametrize("B,K,scale", [(4096, 2, 0.5), (1024, 4, 16.0), (512, 1, 0.5)])
+@pytest.mark.parametrize("B,K,scale", [(4096, 2, 0.5), (1024, 4, 16.0), (512, 1, 0.5),
+                                     (768, 8, 16.0), (512, 5, 0.5)])
 def test_merged_forward_matches_per_model(cuda, B, K, scale):
     """rn_field_fwd_merged (chunks of rays, models' tiles interleaved; encoded
     in merged order or per tile) vs rn_field_fwd: identical per-sample
@@ -212,7 +213,7 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd, r.merged_encode = K <= 4, K > 1
+    r.merged_fwd, r.merged_encode = K <= 8, K > 1
     for o2 in outs[1:]:
         for a, b in zip(outs[0], o2):
             assert torch.equal(a, b)
