@@ -116,8 +116,9 @@ class FusedMLRenderer:
         self.feat_cache = True      # field fwd stores the encoding, bwd skips the re-gather
         # backward scatters the K models' grid gradients merged per ray
         # (rn_field_bwd_merged); False: one model per block (rn_field_bwd)
-        # (K = 1 has nothing to merge: the per-model kernel is 3 % faster there)
-        self.merged_bwd = 1 < model.size <= 8      # rn_field_bwd_merged: K <= 8
+        # (K = 1 too: its row-lane walk beats the per-model kernel, step 3.60 vs
+        # 3.74 ms, profiles/r01/step_variants_k1.json)
+        self.merged_bwd = 1 <= model.size <= 8      # rn_field_bwd_merged: K <= 8
         # forward evaluating the K models' tiles of a chunk interleaved
         # (rn_field_fwd_merged, K <= 8; bit-exact with rn_field_fwd).  One
         # block per CU keeps a chunk's rays in that CU's L1, so the second
@@ -125,7 +126,8 @@ class FusedMLRenderer:
         # before the merged-order encode (tools/fwd_blocks_sweep.py; 2 blocks
         # per CU 1.17, 3 x 4 waves 1.35)
         # (K > 4: the MLP fragments are read from global memory instead of LDS)
-        self.merged_fwd = model.size <= 8
+        # (K = 1: the per-model kernel, 3.72 vs 3.74 ms per step)
+        self.merged_fwd = 1 < model.size <= 8
         # merged forward: encode each chunk in merged (ray, t, model) order
         # first (tiles mixing the sub-NeRFs of a ray stretch share more grid
         # lines: 20.9 vs 28.2 per sample, tools/fwd_lines_sim.py), then the

@@ -138,7 +138,7 @@ def _merged_vs_split(cuda, B, K, scale, p=0.5):
         r.merged_bwd = merged
         _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
         out.append(gr)
-    r.merged_bwd = K > 1
+    r.merged_bwd = 1 <= K <= 8
     return r, out
 
 
@@ -213,7 +213,7 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd, r.merged_encode = K <= 8, K > 1
+    r.merged_fwd, r.merged_encode = 1 < K <= 8, K > 1
     for o2 in outs[1:]:
         for a, b in zip(outs[0], o2):
             assert torch.equal(a, b)
