@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--train-step", type=int, default=1,
                     help="also time the full train step (loss + Adam); 0 = skip")
+    ap.add_argument("--dropin-step", type=int, default=1,
+                    help="also time the step through the drop-in rendering.ml_render chain; 0 = skip")
     ap.add_argument("--split-bwd", action="store_true",
                     help="backward with one model per block (rn_field_bwd) instead of the "
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
@@ -222,6 +224,33 @@ def main():
         train = {"value": round(int(tr_acc) / float(tr_el) / 1e6, 2), "unit": "Msamples/s",
                  "ms_per_step": round(float(tr_el) / args.steps * 1e3, 4),
                  "includes": "render + fused loss + backward + FusedAdam"}
+    # the same step through the drop-in path (rendering.ml_render: the
+    # reference's op-by-op autograd structure, vren ops + field autograd on the
+    # same kernels), for the callers that keep ml_rendering.py; rank 0 at N=1.
+    # Same rays and noise cycle as the headline, so the same samples per step.
+    dropin = None
+    if args.dropin_step and world == 1:
+        from radnerf_amd.rendering import ml_render
+
+        def dstep(i):
+            model.zero_grad(set_to_none=True)
+            gate.zero_grad(set_to_none=True)
+            res = ml_render(model, gate, rays_o, rays_d, rays_d, noise=noises[i % 4],
+                            exp_step_factor=esf)
+            torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
+                                    [g_rgb, g_op, g_depth])
+
+        for i in range(2):
+            dstep(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            dstep(i)
+        torch.cuda.synchronize()
+        d_el = time.perf_counter() - t0
+        dropin = {"value": round(int(samples_acc) / d_el / 1e6, 2), "unit": "Msamples/s",
+                  "ms_per_step": round(d_el / args.steps * 1e3, 4),
+                  "path": "rendering.ml_render (drop-in autograd chain), fwd+bwd"}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:
@@ -294,6 +323,7 @@ def main():
                "rgb_linf_vs_ref": rgb_linf,
                "forward_only": fwd_only,
                "train_step": train,
+               "dropin_step": dropin,
                # MFMA use: algorithmic MLP flops (56,832 per sample
                # fwd+bwd, unpadded) at `value`, against the dense f16 peak
                "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),
