@@ -18,19 +18,31 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"field_bwd": "k_field_bwd", "field_fwd": "k_field_fwd"}
+# the fused chain's kernels; the per-model kernels only where a run has no
+# merged launch (--split-bwd), never mixed (bench.py's drop-in leg runs them)
+KERNELS = {"field_bwd": ("k_field_bwd_merged", "k_field_bwd"),
+           "field_fwd": ("k_field_fwd_merged", "k_field_fwd")}
 
 
 def per_dispatch(d):
     path = os.path.join(d, "run_counter_collection.csv")
-    vals = defaultdict(lambda: defaultdict(float))   # kernel -> dispatch -> value
+    vals = defaultdict(lambda: defaultdict(float))   # (kernel, pattern) -> dispatch -> value
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
-            for key, pat in KERNELS.items():
-                if pat in name:
-                    vals[key][row["Dispatch_Id"]] += float(row["Counter_Value"])
-    return {k: sum(v.values()) / len(v) for k, v in vals.items() if v}
+            for key, pats in KERNELS.items():
+                for pat in pats:
+                    if pat + "<" in name or pat + "(" in name:
+                        vals[(key, pat)][row["Dispatch_Id"]] += float(row["Counter_Value"])
+                        break
+    out = {}
+    for key, pats in KERNELS.items():
+        for pat in pats:
+            v = vals.get((key, pat))
+            if v:
+                out[key] = sum(v.values()) / len(v)
+                break
+    return out
 
 
 def main():
