@@ -193,7 +193,7 @@ def main():
         params = [model.xyz_encoder.params, model.mlp_params, gate.params]
         for p_, v_ in zip(params, ar.views):
             p_.grad = v_
-        opt = FusedAdam(params, lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+        opt = FusedAdam(params, lr=1e-2, eps=1e-15)   # train_ml.py:143 (apex defaults)
         tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(7 + rank)).to(dev)
 
         def tstep(i):

@@ -275,14 +275,17 @@ int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
  * divide by the element counts for the reference's per-term means.  Seeds:
  * the gradients of sum(term.mean()) w.r.t. rgb, opacity, depth and gate.
  * rn_adam: torch.optim.Adam step (train_ml.py:138-153, apex FusedAdam with
- * eps 1e-15) over n fp32 params; optional f16 mirror of params[0, n_f16).   */
+ * eps 1e-15) over n fp32 params; optional f16 mirror of params[0, n_f16).
+ * The hyper-parameters are doubles: the step constants (1-beta, lr/bc1,
+ * sqrt(bc2)) are formed in double on the host, as torch does, then rounded
+ * once to fp32.                                                              */
 int rn_nerf_loss(const float* rgb, const float* target_rgb, const float* opacity,
                  const float* depth, const float* gate, const float* importance, int64_t n_rays,
                  int32_t n_models, float lambda_opacity, float lambda_cv, float lambda_dm,
                  float* loss_out, float* dL_drgb, float* dL_dopacity, float* dL_ddepth,
                  float* dL_dgate, void* stream);
 int rn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-            float lr, float beta1, float beta2, float eps, int32_t step, float grad_scale,
+            double lr, double beta1, double beta2, double eps, int32_t step, float grad_scale,
             void* params_f16, int64_t n_f16, void* stream);
 
 /* rn_get_rays: train_ml.py:84-96 + ray_utils.py:45-70 for a batch of picks.

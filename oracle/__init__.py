@@ -36,6 +36,8 @@ def lib():
         _lib.oracle_ml_march.restype = ctypes.c_int64
         _lib.oracle_morton3d_one.restype = ctypes.c_uint32
         _lib.oracle_morton3d_invert_one.restype = ctypes.c_uint32
+        _lib.oracle_det_expf.restype = ctypes.c_float
+        _lib.oracle_det_expf.argtypes = [ctypes.c_float]
     return _lib
 
 
@@ -50,6 +52,13 @@ def _f32(a):
 I64 = ctypes.c_int64
 I32 = ctypes.c_int32
 F32 = ctypes.c_float
+
+
+def det_expf(x):
+    """The compositing exponent (vren_oracle.c det_expf), elementwise."""
+    f = lib().oracle_det_expf
+    x = np.asarray(x, np.float32).reshape(-1)
+    return np.array([f(float(v)) for v in x], np.float32)
 
 
 def morton3d(coords):

@@ -3,10 +3,18 @@ field and gate (models/networks.py:214-328 MNGP, :1070-1093 Ray_Gate) with the
 tinycudann semantics of networks.py:229-289 (hash grid L=16 F=2, SH degree 4,
 FullyFusedMLP without bias).  Autograd provides the backward reference.
 
-f16 rounding points are the ones the HIP kernels use (DESIGN.md §field):
-weights f16; encoding, hidden activations and geo output rounded to f16;
-sigma = exp(f16 geo output 0); rgb = f16(sigmoid(fp32 pre-activation)); gate
-logits f16, softmax fp32.  tcnn is an absent, unpinned dependency, so this
+f16 rounding points are the ones the HIP kernels use (DESIGN.md §2):
+weights f16; encoding, hidden activations and geo outputs 1..16 rounded to f16;
+sigma = exp(fp32 geo output 0); rgb = sigmoid(fp32 pre-activation) in fp32;
+gate input and weights f16, hidden activations / logits fp32, softmax fp32.
+
+Deviation from tcnn's own numerics (wider everywhere, allowed by north_star):
+upstream tiny-cuda-nn accumulates the 8-corner trilinear sum in __half
+(`result` of type T in kernel_grid), runs FullyFusedMLP with half accumulator
+fragments, emits the network output (sigma pre-activation, rgb) as f16, and
+accumulates the grid gradient with half2 atomics.  This restatement (and the
+HIP kernels) accumulate the trilinear sum, every MLP layer and the grid
+gradient in fp32, and keep sigma / rgb in fp32.  tcnn is an absent, unpinned dependency, so this
 restatement is "parity unpinned" against tcnn itself.
 """
 import math
@@ -150,21 +158,25 @@ def field_forward(x, d, grid_params, mlp, lv, xyz_min, xyz_max):
     e = r16(hash_encode(u, grid_params, lv))
     W = {k: r16(v) for k, v in mlp.items()}
     h1 = r16(torch.relu(e @ W["g1"].t()))
-    g = r16(h1 @ W["g2"].t())
-    sigma = TruncExp.apply(g[:, 0])
+    g32 = h1 @ W["g2"].t()
+    g = r16(g32)
+    sigma = TruncExp.apply(g32[:, 0])
     sh = r16(sh4(d))
     r1 = r16(torch.relu(torch.cat([sh, g[:, 1:]], 1) @ W["r1"].t()))
     r2 = r16(torch.relu(r1 @ W["r2"].t()))
     out = r2 @ W["r3"].t()
-    rgb = r16(torch.sigmoid(out))
+    rgb = torch.sigmoid(out)
     return sigma, rgb
 
 
 def gate_forward(x6, gate_w):
-    """Ray_Gate.forward: softmax(MLP(x6)), tcnn f16 MLP -> f16 logits -> fp32 softmax."""
+    """Ray_Gate.forward: softmax(MLP(x6)) with f16 input and weights (tcnn) and
+    fp32 hidden activations / logits.  tcnn rounds those to f16; at scale 16
+    (|rays_o| up to 24) a rounding flip moves the gate by ~2e-3 against any
+    other accumulation order, so both sides evaluate them wider."""
     W = {k: r16(v) for k, v in gate_w.items()}
     h = r16(x6)
     for n in ("w0", "w1", "w2", "w3"):
-        h = r16(torch.relu(h @ W[n].t()))
-    logit = r16(h @ W["w4"].t())
+        h = torch.relu(h @ W[n].t())
+    logit = h @ W["w4"].t()
     return torch.softmax(logit, 1)

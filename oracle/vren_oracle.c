@@ -13,6 +13,9 @@
  * Contraction policy: compiled with -ffp-contract=off; the
  * multiply-adds that nvcc fuses in the reference are explicit fmaf() calls at
  * exactly the sites the HIP kernels use them.
+ * Threads: rays (segments) are independent, so march and composite loops run
+ * under OpenMP (OMP_NUM_THREADS); the march counts first, takes ray-order
+ * starts serially, then writes.  Results do not depend on the thread count.
  * Ordering: the reference allocates sample slots with atomicAdd
  * (raymarching.cu:237-238), so its row order is nondeterministic; this oracle
  * uses ray order with start = exclusive prefix of the per-ray counts.
@@ -28,6 +31,31 @@
 static float clampf_(float f, float a, float b) { return fmaxf(a, fminf(f, b)); }
 /* raymarching.cu:7 */
 static float signf_(float x) { return copysignf(1.0f, x); }
+
+/* exp(x) as one fixed sequence of IEEE-754 single operations: the
+ * compositing exponent of volumerendering.cu:31 (`__expf(-sigma*delta)`, CUDA's
+ * ex2.approx) restated with a formulation the GPU kernels evaluate with the
+ * same operations, so transmittance and the early-termination sample match
+ * bit for bit.  Range reduction x = k*ln2 + r (Cody-Waite: 15-bit head + tail),
+ * degree-7 Taylor polynomial in Horner form with fmaf, exact ldexpf.
+ * Within 1 ulp of exp for x in [-87, 0]. */
+float oracle_det_expf(float x);
+static float det_expf(float x) {
+    if (!(x >= -87.0f)) return x != x ? x : 0.0f;
+    if (x > 88.0f) return INFINITY;
+    const float k = rintf(x * 1.44269502162933349609375f);
+    float r = fmaf(k, -0.693145751953125f, x);
+    r = fmaf(k, -1.428606765330187045037746429443359375e-06f, r);
+    float p = 1.98412701138295233249664306640625e-04f;
+    p = fmaf(p, r, 1.388888922519981861114501953125e-03f);
+    p = fmaf(p, r, 8.333333767950534820556640625e-03f);
+    p = fmaf(p, r, 4.16666679084300994873046875000e-02f);
+    p = fmaf(p, r, 1.66666671633720397949218750000e-01f);
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return ldexpf(p, (int)k);
+}
 /* raymarching.cu:11-13 */
 static float calc_dt(float t, float esf, int max_samples, int grid_size, float scale) {
     return clampf_(t * esf, SQRT3 / max_samples, SQRT3 * 2 * scale / grid_size);
@@ -186,19 +214,33 @@ int64_t oracle_raymarching_train(const float* rays_o, const float* rays_d, const
                                  int64_t n_rays, int64_t cap, int64_t* rays_a, float* xyzs,
                                  float* dirs, float* deltas, float* ts) {
     cfg_t c = {cascades, grid_size, max_samples, scale, scale, esf};
-    int64_t start = 0;
+    /* pass 1 (rays independent: OpenMP over rays), count */
+#pragma omp parallel for schedule(dynamic, 16)
     for (int64_t r = 0; r < n_rays; ++r) {
         float t1 = hits_t[2 * r], t2 = hits_t[2 * r + 1];
         if (t1 >= 0) {  /* raymarching.cu:195-198 */
             const float dt = calc_dt(t1, esf, max_samples, grid_size, scale);
             t1 = fmaf(dt, noise[r], t1);
         }
-        const int n = march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 1, 0, 0, 0, 0, 0);
-        rays_a[3 * r] = r; rays_a[3 * r + 1] = start; rays_a[3 * r + 2] = n;
-        if (n > 0 && start + n <= cap)
-            march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 0, n, xyzs + 3 * start,
-                  dirs + 3 * start, ts + start, deltas + start);
-        start += n;
+        rays_a[3 * r] = r;
+        rays_a[3 * r + 2] = march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 1, 0, 0, 0, 0, 0);
+    }
+    /* ray-order starts (the reference's atomicAdd order is nondeterministic) */
+    int64_t start = 0;
+    for (int64_t r = 0; r < n_rays; ++r) { rays_a[3 * r + 1] = start; start += rays_a[3 * r + 2]; }
+    /* pass 2, write */
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t r = 0; r < n_rays; ++r) {
+        const int64_t s0 = rays_a[3 * r + 1];
+        const int n = (int)rays_a[3 * r + 2];
+        if (n == 0 || s0 + n > cap) continue;
+        float t1 = hits_t[2 * r], t2 = hits_t[2 * r + 1];
+        if (t1 >= 0) {
+            const float dt = calc_dt(t1, esf, max_samples, grid_size, scale);
+            t1 = fmaf(dt, noise[r], t1);
+        }
+        march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 0, n, xyzs + 3 * s0,
+              dirs + 3 * s0, ts + s0, deltas + s0);
     }
     return start;
 }
@@ -257,6 +299,7 @@ void oracle_composite_train_fw(const float* sig, const float* rgbs, const float*
                                const float* ts, const int64_t* rays_a, int64_t n_rows, float thr,
                                int64_t* total, float* opacity, float* depth, float* rgb,
                                float* ws) {
+#pragma omp parallel for schedule(dynamic, 16)
     for (int64_t n = 0; n < n_rows; ++n) {
         const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
         const int N = (int)rays_a[3 * n + 2];
@@ -264,7 +307,7 @@ void oracle_composite_train_fw(const float* sig, const float* rgbs, const float*
         float T = 1.0f;
         while (samples < N) {
             const int64_t s = start + samples;
-            const float a = 1.0f - expf(-sig[s] * dl[s]);
+            const float a = 1.0f - det_expf(-sig[s] * dl[s]);
             const float w = a * T;
             rgb[3 * ray] = fmaf(w, rgbs[3 * s], rgb[3 * ray]);
             rgb[3 * ray + 1] = fmaf(w, rgbs[3 * s + 1], rgb[3 * ray + 1]);
@@ -287,6 +330,7 @@ void oracle_composite_train_bw(const float* gO, const float* gD, const float* gR
                                const int64_t* rays_a, int64_t n_rows, const float* opacity,
                                const float* depth, const float* rgb, float thr, float* dsig,
                                float* drgb) {
+#pragma omp parallel for schedule(dynamic, 16)
     for (int64_t n = 0; n < n_rows; ++n) {
         const int64_t ray = rays_a[3 * n], start = rays_a[3 * n + 1];
         const int N = (int)rays_a[3 * n + 2];
@@ -301,7 +345,7 @@ void oracle_composite_train_bw(const float* gO, const float* gD, const float* gR
         int samples = 0;
         while (samples < N) {
             const int64_t s = start + samples;
-            const float a = 1.0f - expf(-sig[s] * dl[s]);
+            const float a = 1.0f - det_expf(-sig[s] * dl[s]);
             const float w = a * T;
             r = fmaf(w, rgbs[3 * s], r); g = fmaf(w, rgbs[3 * s + 1], g);
             b = fmaf(w, rgbs[3 * s + 2], b); d = fmaf(w, ts[s], d);
@@ -328,13 +372,14 @@ void oracle_composite_test_fw(const float* sig, const float* rgbs, const float* 
                               const float* ts, int64_t n_alive, int n_samples, int64_t* alive,
                               float thr, const int32_t* n_eff, float* opacity, float* depth,
                               float* rgb) {
+#pragma omp parallel for schedule(dynamic, 16)
     for (int64_t n = 0; n < n_alive; ++n) {
         if (n_eff[n] == 0) { alive[n] = -1; continue; }
         const int64_t r = alive[n];
         float T = 1 - opacity[r];
         for (int s = 0; s < n_eff[n]; ++s) {
             const int64_t o = n * n_samples + s;
-            const float a = 1.0f - expf(-sig[o] * dl[o]);
+            const float a = 1.0f - det_expf(-sig[o] * dl[o]);
             const float w = a * T;
             rgb[3 * r] = fmaf(w, rgbs[3 * o], rgb[3 * r]);
             rgb[3 * r + 1] = fmaf(w, rgbs[3 * o + 1], rgb[3 * r + 1]);
@@ -357,28 +402,39 @@ int64_t oracle_ml_march(const float* rays_o, const float* rays_d, const float* c
                         int64_t cap, int32_t* counts, int64_t* starts, float* xyzs, float* ts,
                         float* deltas) {
     cfg_t c = {cascades, grid_size, max_samples, scale, scale, esf};
-    int64_t start = 0;
-    for (int k = 0; k < K; ++k) {
-        for (int64_t r = 0; r < n_rays; ++r) {
+    const int64_t n_seg = (int64_t)K * n_rays;
+    if (n_seg == 0) return 0;
+    /* pass 1 (segments independent: OpenMP), count; pass 2, write */
+    for (int pass = 0; pass < 2; ++pass) {
+#pragma omp parallel for schedule(dynamic, 16)
+        for (int64_t g = 0; g < n_seg; ++g) {
+            const int k = (int)(g / n_rays);
+            const int64_t r = g - (int64_t)k * n_rays;
+            if (pass == 1 && (counts[g] == 0 || starts[g] + counts[g] > cap)) continue;
             float t1, t2;
             aabb_one(rays_o + 3 * r, rays_d + 3 * r, center, half_size, &t1, &t2);
             if (!(t2 > 0)) { t1 = -1.f; t2 = -1.f; }
             else { t1 = fmaxf(t1, 0.0f); if (t1 < near_distance) t1 = near_distance; }
-            const int64_t g = (int64_t)k * n_rays + r;
             if (t1 >= 0) {
                 const float dt = calc_dt(t1, esf, max_samples, grid_size, scale);
                 t1 = fmaf(dt, noise[g], t1);
             }
             const uint8_t* bits = bitfields + k * bitfield_bytes;
-            const int n = march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 1, 0, 0, 0, 0, 0);
-            counts[g] = n; starts[g] = start;
-            if (n > 0 && start + n <= cap)
-                march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 0, n, xyzs + 3 * start, 0,
-                      ts + start, deltas + start);
-            start += n;
+            if (pass == 0) {
+                counts[g] = march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 1, 0, 0, 0, 0, 0);
+            } else {
+                const int64_t s0 = starts[g];
+                march(rays_o + 3 * r, rays_d + 3 * r, t1, t2, bits, &c, 0, counts[g], xyzs + 3 * s0,
+                      0, ts + s0, deltas + s0);
+            }
+        }
+        if (pass == 0) {
+            int64_t start = 0;
+            for (int64_t g = 0; g < n_seg; ++g) { starts[g] = start; start += counts[g]; }
+            if (cap == 0) return start;
         }
     }
-    return start;
+    return starts[n_seg - 1] + counts[n_seg - 1];
 }
 
 /* intersection.cu:103-120 (_ray_sphere_intersect) + :123-150 (kernel) + :191-195
@@ -486,3 +542,6 @@ void oracle_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, c
         for (int c = 0; c < 3; ++c) { dL_drays_o[3 * n + c] = o[c]; dL_drays_d[3 * n + c] = d[c]; }
     }
 }
+
+/* the compositing exponent, exported for tests/test_oracle.py's accuracy check */
+float oracle_det_expf(float x) { return det_expf(x); }

@@ -16,6 +16,19 @@ namespace {
 
 struct SegOut { float O, D, R, G, B; int used; };
 
+// the chunk's early-termination lane (or -1), bit-exact against the serial
+// fold: rn_chunk_break, with the whole-segment serial fold when ambiguous
+__device__ __forceinline__ int seg_break(const float* __restrict__ sig,
+                                         const float* __restrict__ dl, int64_t start, int n,
+                                         int base, float pin, bool valid, float thr) {
+    int brk = rn_chunk_break(pin, valid, base + rn_lane(), thr);
+    if (brk == -2) {
+        const int b = rn_serial_break(sig, dl, start, n, thr);
+        brk = (b >= base && b < base + RN_WAVE) ? b - base : -1;
+    }
+    return brk;
+}
+
 // Forward over one segment.  All lanes of the wave call this with the same
 // (start, n).  Writes ws for the samples that contribute (<= break sample).
 __device__ SegOut seg_forward(const float* __restrict__ sig, const float* __restrict__ rgbs,
@@ -36,7 +49,7 @@ __device__ SegOut seg_forward(const float* __restrict__ sig, const float* __rest
         float a = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, t = 0.f;
         if (valid) {
             const int64_t s = start + i;
-            a = 1.0f - __expf(-sig[s] * dl[s]);
+            a = 1.0f - rn_exp_det(-sig[s] * dl[s]);
             c0 = rgbs[3 * s]; c1 = rgbs[3 * s + 1]; c2 = rgbs[3 * s + 2]; t = ts[s];
         }
         const float om = 1.0f - a;
@@ -44,10 +57,10 @@ __device__ SegOut seg_forward(const float* __restrict__ sig, const float* __rest
         const float pin = rn_wave_incl_prod(lane == 0 ? T * om : om);
         const float pex = rn_wave_shr1(pin, T);
         const float w = a * pex;
-        const unsigned long long stop = __ballot(valid && pin <= thr);
         int last = RN_WAVE - 1;
-        if (stop) {
-            last = __ffsll((long long)stop) - 1;
+        const int brk = seg_break(sig, dl, start, n, base, pin, valid, thr);
+        if (brk >= 0) {
+            last = brk;
             used = base + last;
             done = true;
         }
@@ -97,7 +110,7 @@ __device__ void seg_backward(const float* __restrict__ sig, const float* __restr
         float a = 0.f, c0 = 0.f, c1 = 0.f, c2 = 0.f, t = 0.f, d = 0.f, gw = 0.f, wsv = 0.f;
         if (valid) {
             d = dl[s];
-            a = 1.0f - __expf(-sig[s] * d);
+            a = 1.0f - rn_exp_det(-sig[s] * d);
             c0 = rgbs[3 * s]; c1 = rgbs[3 * s + 1]; c2 = rgbs[3 * s + 2]; t = ts[s];
             if (dL_dws) { gw = dL_dws[s]; wsv = ws[s]; }
         }
@@ -105,8 +118,9 @@ __device__ void seg_backward(const float* __restrict__ sig, const float* __restr
         const float pin = rn_wave_incl_prod(lane == 0 ? T * om : om);
         const float pex = rn_wave_shr1(pin, T);
         const float w = a * pex;
-        const unsigned long long stop = __ballot(valid && pin <= thr);
-        const int last = stop ? __ffsll((long long)stop) - 1 : RN_WAVE - 1;
+        const int brk = seg_break(sig, dl, start, n, base, pin, valid, thr);
+        const bool stop = brk >= 0;
+        const int last = stop ? brk : RN_WAVE - 1;
         const bool live = valid && lane <= last;
         // inclusive prefix sums (r, g, b, d accumulate before the gradient)
         const float sr = pr + rn_wave_incl_sum(live ? w * c0 : 0.f);
@@ -191,7 +205,7 @@ k_composite_test(int n_alive, int n_samples, const float* __restrict__ sig,
     const size_t row = (size_t)n * n_samples;
     for (int s = 0; s < n_eff[n]; ++s) {
         const size_t o = row + s;
-        const float a = 1.0f - __expf(-sig[o] * dl[o]);
+        const float a = 1.0f - rn_exp_det(-sig[o] * dl[o]);
         const float w = a * T;
         cr = fmaf(w, rgbs[3 * o], cr); cg = fmaf(w, rgbs[3 * o + 1], cg);
         cb = fmaf(w, rgbs[3 * o + 2], cb);

@@ -338,7 +338,7 @@ struct FwdState {
     half8 gin;             // geo outputs 1..16 (f16) = rgb-net input k-step 1
     half8 sh;              // SH (f16)             = rgb-net input k-step 0
     half8 r1[4], r2[4];    // rgb hidden
-    float g0;              // geo output 0 (f16-rounded), lanes h == 0
+    float g0;              // geo output 0 (fp32 accumulator), lanes h == 0
     f32x16 out;            // rgb pre-activation (rows 0..2 on lanes h == 0)
 };
 
@@ -356,7 +356,9 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
     for (int q = 0; q < 4; ++q) g = rn_mfma(rn_frag(W, 4 + q), st.h1[q], g);
     half8 gk1;
     rn_acc_to_frags<false>(g, st.gin, gk1);
-    st.g0 = (float)gk1[0];
+    // sigma = TruncExp(h0) from the fp32 accumulator (wider than tcnn's f16
+    // output; acc reg 8 of lanes h == 0 is row 16 = geo output 0)
+    st.g0 = g[8];
     // rgb layer 1: [SH | geo 1..16] -> 64
     a0 = rn_zero16(); a1 = rn_zero16();
     a0 = rn_mfma(rn_frag(W, 8), st.sh, a0); a0 = rn_mfma(rn_frag(W, 9), st.gin, a0);
@@ -378,7 +380,7 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
     for (int q = 0; q < 4; ++q) st.out = rn_mfma(rn_frag(W, 20 + q), st.r2[q], st.out);
 }
 
-__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2,
        CACHE_READ_NT = 3 };   // READ past L1: written by other waves of this kernel
@@ -463,12 +465,13 @@ k_field_fwd(FieldArgs a) {
         bool valid; int64_t s; float ux, uy, uz;
         tile_forward<MODE, CACHE>(a, sT, sW, base, n, tile, st, valid, s, ux, uy, uz);
         if (valid && h == 0) {
-            // TruncExp.forward on the f16 geo output (custom_functions.py:165-167)
+            // TruncExp.forward on geo output 0 (custom_functions.py:165-167)
             a.sigma[s] = expf(st.g0);
-            // Sigmoid output activation, tcnn f16 output
-            a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
-            a.rgb[3 * s + 1] = (float)(rn_half)sigmoidf(st.out[1]);
-            a.rgb[3 * s + 2] = (float)(rn_half)sigmoidf(st.out[2]);
+            // Sigmoid output activation in fp32 (tcnn rounds it to f16; the
+            // wider output keeps one f16 ulp of rgb off the ray colour)
+            a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
+            a.rgb[3 * s + 1] = sigmoidf(st.out[1]);
+            a.rgb[3 * s + 2] = sigmoidf(st.out[2]);
         }
     }
 }
@@ -956,30 +959,42 @@ __device__ __forceinline__ void dw_flush(const f32x16& acc, float* dw, int off, 
 }
 
 // flush a wave's owned dW tiles (ownership table in k_field_bwd) into dw
+// accA holds rgb-net tiles (at the rgb chain's scale), accB geo-net tiles
+// (at the geo chain's scale); a zero scale means "empty"
+struct DwScale { float a, b; };
+
 __device__ __forceinline__ void dw_flush_owned(const f32x16& accA, const f32x16& accB, float* dw,
-                                               int wid, float inv) {
+                                               int wid, DwScale sc) {
+    const float ia = sc.a != 0.f ? 1.0f / sc.a : 0.f, ib = sc.b != 0.f ? 1.0f / sc.b : 0.f;
     if (wid < 2) {
-        dw_flush<DW_ROWS_LT3>(accA, dw, 9280, 64, 0, 32 * wid, inv);   // rgb3
-        dw_flush<DW_GEO>(accB, dw, 2048, 64, 0, 32 * wid, inv);        // geo2
+        if (ia != 0.f) dw_flush<DW_ROWS_LT3>(accA, dw, 9280, 64, 0, 32 * wid, ia);   // rgb3
+        if (ib != 0.f) dw_flush<DW_GEO>(accB, dw, 2048, 64, 0, 32 * wid, ib);        // geo2
     } else if (wid < 6) {
         const int mm = (wid - 2) >> 1, nn = (wid - 2) & 1;
-        dw_flush<DW_PLAIN>(accA, dw, 5184, 64, 32 * mm, 32 * nn, inv); // rgb2
-        if (wid < 4) dw_flush<DW_PLAIN>(accB, dw, 0, 32, 32 * (wid - 2), 0, inv);  // geo1
+        if (ia != 0.f) dw_flush<DW_PLAIN>(accA, dw, 5184, 64, 32 * mm, 32 * nn, ia); // rgb2
+        if (wid < 4 && ib != 0.f)
+            dw_flush<DW_PLAIN>(accB, dw, 0, 32, 32 * (wid - 2), 0, ib);              // geo1
     } else {
-        dw_flush<DW_PLAIN>(accA, dw, 3136, 32, 32 * (wid - 6), 0, inv); // rgb1
+        if (ia != 0.f) dw_flush<DW_PLAIN>(accA, dw, 3136, 32, 32 * (wid - 6), 0, ia); // rgb1
     }
 }
 
 // Backward of one block iteration (8 waves x 32-sample tiles, the tiles'
-// forward state in `st`): seeds -> block gradient scale -> dX chain on MFMA
-// with the block-cooperative dW tiles (accA/accB at cur_scale, rescaled
-// exactly when the scale changes).  Returns dL/dencoding at scale `gscale`
+// forward state in `st`): seeds -> block gradient scales -> dX chain on MFMA
+// with the block-cooperative dW tiles (accA / accB at cur.a / cur.b, rescaled
+// exactly when a scale changes).  Returns dL/dencoding at scale `gscale`
 // (rows in MFMA accumulator order); zero_iter: all 256 seeds are zero.
+// Two power-of-two scales: the rgb chain (rgb3 -> rgb1) is scaled by the
+// block's largest rgb seed, the geo chain (geo2 -> encoding) by the largest
+// of all seeds.  With one shared scale, a sub-NeRF whose gate weight is ~0 has
+// rgb seeds ~1e-8 of its sigma seeds, and its rgb-net gradients fall below
+// f16's range (tcnn's global loss scale flushes them to zero); the rgb-path
+// rows of dL/dgeo are brought to the geo scale in fp32 before the f16 cast.
 __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* sW,
                                              const rn_half* sImg, float* sMax, rn_half* imgY,
                                              rn_half* imgX, FwdState& st, bool valid, int64_t s,
                                              int wid, f32x16& accA, f32x16& accB,
-                                             float& cur_scale, bool do_dw, float& gscale_out,
+                                             DwScale& cur, bool do_dw, float& gscale_out,
                                              bool& zero_iter_out) {
     const int lane = rn_lane(), h = lane >> 5;
     const half8 z8 = rn_zero8();
@@ -995,30 +1010,38 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         // TruncExp.backward: g * exp(clamp(x, -15, 15))  (custom_functions.py:171-173)
         gsig = ds * expf(fminf(fmaxf(st.g0, -15.f), 15.f));
     }
-    float m = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fmaxf(fabsf(o2), fabsf(gsig)));
+    float mr = fmaxf(fmaxf(fabsf(o0), fabsf(o1)), fabsf(o2)), mg = fabsf(gsig);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    if (lane == 0) sMax[wid] = m;
+    for (int off = 32; off > 0; off >>= 1) {
+        mr = fmaxf(mr, __shfl_xor(mr, off));
+        mg = fmaxf(mg, __shfl_xor(mg, off));
+    }
+    if (lane == 0) { sMax[2 * wid] = mr; sMax[2 * wid + 1] = mg; }
     __syncthreads();                                                    // B0
-    float bm = sMax[0];
+    float bmr = sMax[0], bmg = sMax[1];
 #pragma unroll
-    for (int w = 1; w < BWD_WAVES; ++w) bm = fmaxf(bm, sMax[w]);
+    for (int w = 1; w < BWD_WAVES; ++w) { bmr = fmaxf(bmr, sMax[2 * w]); bmg = fmaxf(bmg, sMax[2 * w + 1]); }
+    const float bm = fmaxf(bmr, bmg);
     // an iteration whose 256 samples all have zero seeds (samples past the
     // early-termination point of their rays, volumerendering.cu:150) adds
     // nothing to the hash grid: its scatter walk is skipped (an early
     // `continue` of the whole iteration made the compiler spill 190 B/lane)
     const bool zero_iter = bm == 0.f;
-    const float gscale = rn_wave_grad_scale(bm);   // uniform over the block
-    if (cur_scale != gscale) {                     // exact power-of-two rescale
-        const float r = cur_scale == 0.f ? 0.f : gscale / cur_scale;
-        accA *= r; accB *= r;
-        cur_scale = gscale;
+    const float gscale = rn_wave_grad_scale(bm);    // geo chain, uniform over the block
+    const float rscale = rn_wave_grad_scale(bmr);   // rgb chain (>= gscale)
+    if (cur.a != rscale) {                          // exact power-of-two rescales
+        accA *= cur.a == 0.f ? 0.f : rscale / cur.a;
+        cur.a = rscale;
+    }
+    if (cur.b != gscale) {
+        accB *= cur.b == 0.f ? 0.f : gscale / cur.b;
+        cur.b = gscale;
     }
     half8 dO = z8;
     if (h == 0) {
-        dO[0] = (rn_half)(o0 * gscale);
-        dO[1] = (rn_half)(o1 * gscale);
-        dO[2] = (rn_half)(o2 * gscale);
+        dO[0] = (rn_half)(o0 * rscale);
+        dO[1] = (rn_half)(o1 * rscale);
+        dO[2] = (rn_half)(o2 * rscale);
     }
     // ---- layer rgb3: dW (w0, w1) = dO x R2 ; dR2 = Wr3^T dO masked
     if (do_dw) {
@@ -1070,6 +1093,7 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         f32x16 b = rn_zero16();
 #pragma unroll
         for (int q = 0; q < 4; ++q) b = rn_mfma(rn_frag(sW, 34 + q), dr1f[q], b);
+        b *= gscale / rscale;                      // rgb-path rows to the geo scale (exact)
         if (h == 0) b[8] = gsig * gscale;          // row 16 = dL/dh0
         rn_acc_to_frags<false>(b, dg0, dg1);
     }
@@ -1113,7 +1137,7 @@ __global__ void __launch_bounds__(BWD_WAVES * 64)
 k_field_bwd(FieldArgs a) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
-    __shared__ float sMax[BWD_WAVES];
+    __shared__ float sMax[2 * BWD_WAVES];
     __shared__ LvTab sT;
     __shared__ uint32_t sRing[BWD_WAVES * SC_STREAMS * 3 * SC_RING];   // scatter rings
     const int k = blockIdx.y;
@@ -1137,7 +1161,7 @@ k_field_bwd(FieldArgs a) {
     //   w0: r3(n=0), g2(n=0)   w1: r3(n=1), g2(n=1)   w2..w5: r2(m,n)
     //   w2: + g1(m=0)          w3: + g1(m=1)          w6, w7: r1(m)
     f32x16 accA = rn_zero16(), accB = rn_zero16();
-    float cur_scale = 0.f;   // scale the accumulators are expressed at (0 = empty)
+    DwScale cur = {0.f, 0.f};   // scales the accumulators are expressed at (0 = empty)
 
     const bool do_sc = !(a.dbg & 4);
     // scatter staging (dL/dfeature rows, unit coords of the iteration's 256
@@ -1161,7 +1185,7 @@ k_field_bwd(FieldArgs a) {
 
         float gscale; bool zero_iter;
         const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid, accA, accB,
-                                     cur_scale, do_dw, gscale, zero_iter);
+                                     cur, do_dw, gscale, zero_iter);
 
         // ---- hash-grid gradient scatter (grid_scatter_block)
         if (do_sc && !zero_iter) {
@@ -1181,8 +1205,7 @@ k_field_bwd(FieldArgs a) {
     }
     if (do_sc) ring_drain(R, 0u, grad_rs, a.dbg);
     // ---- flush the owned dW tiles
-    if (cur_scale != 0.f && do_dw) dw_flush_owned(accA, accB, a.dw + (size_t)k * FIELD_PARAMS, wid,
-                                                   1.0f / cur_scale);
+    if (do_dw) dw_flush_owned(accA, accB, a.dw + (size_t)k * FIELD_PARAMS, wid, cur);
 }
 
 // ---------------------------------------------------------------------------
@@ -1244,15 +1267,15 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
     }
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
-    __shared__ float sMax[BWD_WAVES];
+    __shared__ float sMax[2 * BWD_WAVES];
     __shared__ LvTab sT;
     __shared__ uint32_t sRing[BWD_WAVES * SC_STREAMS * 3 * SC_RING];
-    __shared__ float sScale[MB_KMAX];           // per model: scale of its parked dW (0 = none)
+    __shared__ DwScale sScale[MB_KMAX];         // per model: scales of its parked dW (0 = none)
     // chunk descriptor: r0, r1, then per model: first sample, count, row offset, segment base
     __shared__ int32_t sCh[2 + 4 * MB_KMAX];
     const int K = m.n_models, B = m.n_rays;
     lv_stage(sT, a.gm);
-    if (threadIdx.x < MB_KMAX) sScale[threadIdx.x] = 0.f;
+    if (threadIdx.x < MB_KMAX) sScale[threadIdx.x] = DwScale{0.f, 0.f};
 
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
@@ -1274,7 +1297,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
                                     (wid - 4) * W2_RING_WORDS;
 
     f32x16 accA = rn_zero16(), accB = rn_zero16();
-    float cur_scale = 0.f;
+    DwScale cur = {0.f, 0.f};
     int cur_k = -1;
     float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
     float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
@@ -1321,13 +1344,14 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
                 __syncthreads();                 // every wave done with sW
                 if (cur_k >= 0) {
                     dw_park(park + (size_t)cur_k * BWD_WAVES * 2048, accA, accB);
-                    if (threadIdx.x == 0) sScale[cur_k] = cur_scale;
+                    if (threadIdx.x == 0) sScale[cur_k] = cur;
                 }
                 rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                                 FIELD_FRAGS * RN_FRAG_BYTES);
                 __syncthreads();
-                cur_scale = sScale[k];
-                if (cur_scale != 0.f) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, accA, accB);
+                cur = sScale[k];
+                if (cur.a != 0.f || cur.b != 0.f)
+                    dw_unpark(park + (size_t)k * BWD_WAVES * 2048, accA, accB);
                 else { accA = rn_zero16(); accB = rn_zero16(); }
                 cur_k = k;
             }
@@ -1343,7 +1367,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
                                          ux, uy, uz);
                 float gscale; bool zero_iter;
                 const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid,
-                                             accA, accB, cur_scale, do_dw, gscale, zero_iter);
+                                             accA, accB, cur, do_dw, gscale, zero_iter);
                 if (valid) {
                     const float ginv = zero_iter ? 0.f : 1.0f / gscale;
                     float* row = rows + (size_t)(roff + i) * MB_ROW;
@@ -1414,11 +1438,12 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
     // ---- flush every model's dW (the current one from registers)
     if (do_dw) {
         for (int k = 0; k < K; ++k) {
-            float sc = sScale[k];
+            DwScale sc = sScale[k];
             f32x16 A, Bm;
-            if (k == cur_k) { sc = cur_scale; A = accA; Bm = accB; }
-            else if (sc != 0.f) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, A, Bm);
-            if (sc != 0.f) dw_flush_owned(A, Bm, a.dw + (size_t)k * FIELD_PARAMS, wid, 1.0f / sc);
+            if (k == cur_k) { sc = cur; A = accA; Bm = accB; }
+            else if (sc.a != 0.f || sc.b != 0.f) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, A, Bm);
+            if (sc.a != 0.f || sc.b != 0.f)
+                dw_flush_owned(A, Bm, a.dw + (size_t)k * FIELD_PARAMS, wid, sc);
         }
     }
 }
@@ -1475,9 +1500,9 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
                               st, ux, uy, uz);
         if (valid && h == 0) {
             a.sigma[s] = expf(st.g0);
-            a.rgb[3 * s + 0] = (float)(rn_half)sigmoidf(st.out[0]);
-            a.rgb[3 * s + 1] = (float)(rn_half)sigmoidf(st.out[1]);
-            a.rgb[3 * s + 2] = (float)(rn_half)sigmoidf(st.out[2]);
+            a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
+            a.rgb[3 * s + 1] = sigmoidf(st.out[1]);
+            a.rgb[3 * s + 2] = sigmoidf(st.out[2]);
         }
     };
     auto mlp_tiles = [&](const int32_t* ch) {

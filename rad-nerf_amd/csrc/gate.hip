@@ -1,5 +1,6 @@
 // Ray gate of Rad-NeRF on gfx950: MLP 6 -> 64 -> 64 -> 64 -> 64 -> K (ReLU,
-// no bias, f16 like tcnn FullyFusedMLP) + softmax, forward and backward.
+// no bias, f16 weights and input like tcnn FullyFusedMLP; hidden activations
+// and logits kept at ~fp32, see gate_split) + softmax, forward and backward.
 //
 // Reference: models/networks.py:1070-1093 (Ray_Gate), call site
 // models/ml_rendering.py:31-36 (input cat(rays_o, rays_d) or cat(rays_o, imgs_d)).
@@ -27,7 +28,25 @@ struct GateArgs {
 
 namespace {
 
+// h: hidden activations (ReLU, f16 head); the forward carries each layer's
+// f16 tail alongside (split precision, below)
 struct GateState { half8 x; half8 h[4][4]; f32x16 logit; };
+
+// fp32 accumulator tile -> ReLU -> head + tail f16 fragments (v = hi + lo to
+// ~2^-22 relative): the next layer runs W.hi + W.lo on MFMA, i.e. fp32
+// activations with f16 weights.  tcnn rounds every hidden activation to f16;
+// at scale 16 (|rays_o| up to 24) the rounding points flip against any
+// other accumulation order and move the gate by ~2e-3, so the gate is
+// evaluated wider than tcnn (north_star allows wider).
+__device__ __forceinline__ void gate_split(const f32x16& acc, half8& h0, half8& h1, half8& l0,
+                                           half8& l1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float v0 = fmaxf(acc[j], 0.f), v1 = fmaxf(acc[8 + j], 0.f);
+        h0[j] = (rn_half)v0; h1[j] = (rn_half)v1;
+        l0[j] = (rn_half)(v0 - (float)h0[j]); l1[j] = (rn_half)(v1 - (float)h1[j]);
+    }
+}
 
 __device__ __forceinline__ void gate_input(const GateArgs& a, int64_t r, bool valid, half8& x) {
     const int lane = rn_lane(), h = lane >> 5;
@@ -47,8 +66,9 @@ __device__ __forceinline__ void gate_forward(const rn_half* W, GateState& st) {
     f32x16 a0 = rn_zero16(), a1 = rn_zero16();
     a0 = rn_mfma(rn_frag(W, 0), st.x, a0);
     a1 = rn_mfma(rn_frag(W, 1), st.x, a1);
-    rn_acc_to_frags<true>(a0, st.h[0][0], st.h[0][1]);
-    rn_acc_to_frags<true>(a1, st.h[0][2], st.h[0][3]);
+    half8 lo[4];
+    gate_split(a0, st.h[0][0], st.h[0][1], lo[0], lo[1]);
+    gate_split(a1, st.h[0][2], st.h[0][3], lo[2], lo[3]);
 #pragma unroll
     for (int L = 1; L < 4; ++L) {
         a0 = rn_zero16(); a1 = rn_zero16();
@@ -56,14 +76,19 @@ __device__ __forceinline__ void gate_forward(const rn_half* W, GateState& st) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             a0 = rn_mfma(rn_frag(W, fb + q), st.h[L - 1][q], a0);
+            a0 = rn_mfma(rn_frag(W, fb + q), lo[q], a0);
             a1 = rn_mfma(rn_frag(W, fb + 4 + q), st.h[L - 1][q], a1);
+            a1 = rn_mfma(rn_frag(W, fb + 4 + q), lo[q], a1);
         }
-        rn_acc_to_frags<true>(a0, st.h[L][0], st.h[L][1]);
-        rn_acc_to_frags<true>(a1, st.h[L][2], st.h[L][3]);
+        gate_split(a0, st.h[L][0], st.h[L][1], lo[0], lo[1]);
+        gate_split(a1, st.h[L][2], st.h[L][3], lo[2], lo[3]);
     }
     st.logit = rn_zero16();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) st.logit = rn_mfma(rn_frag(W, 26 + q), st.h[3][q], st.logit);
+    for (int q = 0; q < 4; ++q) {
+        st.logit = rn_mfma(rn_frag(W, 26 + q), st.h[3][q], st.logit);
+        st.logit = rn_mfma(rn_frag(W, 26 + q), lo[q], st.logit);
+    }
 }
 
 // softmax over the K logit rows of this lane's sample (rows spread over the
@@ -76,7 +101,7 @@ __device__ __forceinline__ f32x16 gate_softmax(const f32x16& logit, int K) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
         const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
-        z[i] = (float)(rn_half)logit[i];   // tcnn f16 output, softmax in f32
+        z[i] = logit[i];   // fp32 logits (tcnn rounds them to f16: wider here), softmax in f32
         if (row < K) m = fmaxf(m, z[i]);
     }
     m = fmaxf(m, __shfl_xor(m, 32));

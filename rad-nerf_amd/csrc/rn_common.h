@@ -172,3 +172,74 @@ __device__ __forceinline__ float rn_wave_last(float v) {
 __device__ __forceinline__ int rn_wave_incl_sum_i(int v) {
     return rn_wave_incl_scan(v, 0, [](int a, int b) { return a + b; }, RnDppI{});
 }
+
+// ---------------------------------------------------------------------------
+// compositing arithmetic shared bit-for-bit with the CPU oracle
+// ---------------------------------------------------------------------------
+// exp(x) as one fixed sequence of IEEE-754 single operations (round to
+// nearest, fused fmaf, exact ldexpf), so that the GPU and the oracle
+// (vren_oracle.c det_expf) produce identical bits.  The reference uses CUDA's
+// __expf (ex2.approx, up to ~2 ulp); this is within 1 ulp of exp on the
+// compositing range x = -sigma*delta <= 0.  Range reduction x = k ln2 + r
+// (Cody-Waite, ln2 split in a 15-bit head and a tail), |r| <= ln2/2, then a
+// degree-7 Taylor polynomial (truncation < 6e-9 relative).
+__device__ __forceinline__ float rn_exp_det(float x) {
+    if (!(x >= -87.0f)) return x != x ? x : 0.0f;     // exp(-87) > FLT_MIN: no denormals
+    if (x > 88.0f) return __builtin_inff();
+    const float k = rintf(x * 1.44269502162933349609375f);          // log2(e) in f32
+    float r = fmaf(k, -0.693145751953125f, x);                      // ln2 head (exact product)
+    r = fmaf(k, -1.428606765330187045037746429443359375e-06f, r);   // ln2 tail
+    float p = 1.98412701138295233249664306640625e-04f;              // 1/5040
+    p = fmaf(p, r, 1.388888922519981861114501953125e-03f);          // 1/720
+    p = fmaf(p, r, 8.333333767950534820556640625e-03f);             // 1/120
+    p = fmaf(p, r, 4.16666679084300994873046875000e-02f);           // 1/24
+    p = fmaf(p, r, 1.66666671633720397949218750000e-01f);           // 1/6
+    p = fmaf(p, r, 0.5f);
+    p = fmaf(p, r, 1.0f);
+    p = fmaf(p, r, 1.0f);
+    return ldexpf(p, (int)k);
+}
+
+// Early termination, bit-exact against the reference's serial fold
+// (volumerendering.cu:39-44: `T *= 1.0f - a; if (T <= T_threshold) break;`,
+// one sample after the other).  The wave forms T with a prefix product
+// (`pin`, tree order), which differs from the serial fold by at most one
+// rounding per factor on each side: |pin / T_serial - 1| <= 2 (pos+1) 2^-24
+// for the sample at segment position pos.  With that margin a lane is
+// "surely past" (pin (1+m) <= thr), "surely not" (pin (1-m) > thr) or
+// ambiguous.  rn_chunk_break returns the first lane that is not surely-not if
+// it is surely past, -1 if every valid lane is surely-not, and -2 if the first
+// candidate is ambiguous (T within ~1e-5 of T_threshold: rare), where the
+// caller folds the segment serially (rn_serial_break).  The weights keep the
+// tree-order T (within the 1e-4 tolerance); only the integer break is exact.
+__device__ __forceinline__ int rn_chunk_break(float pin, bool valid, int pos, float thr) {
+    const float m = (float)(pos + 2) * 2.384185791015625e-07f;     // 4 ulps per factor
+    const bool cand = valid && pin * (1.0f - m) <= thr;
+    const unsigned long long cb = __ballot(cand);
+    if (!cb) return -1;
+    const int l = __ffsll((long long)cb) - 1;
+    const unsigned long long sure = __ballot(cand && pin * (1.0f + m) <= thr);
+    return ((sure >> l) & 1ull) ? l : -2;
+}
+
+// Serial fold of a whole segment (the reference's order, same exponent):
+// index of the sample whose product first reaches <= thr, or n if none.
+// Lane j of a chunk folds after lanes < j (readlane chain); only called for
+// the ambiguous chunks of rn_chunk_break.
+__device__ __noinline__ int rn_serial_break(const float* __restrict__ sig,
+                                            const float* __restrict__ dl, int64_t start, int n,
+                                            float thr) {
+    const int lane = rn_lane();
+    float t = 1.0f;
+    for (int base = 0; base < n; base += RN_WAVE) {
+        const int i = base + lane;
+        float om = 1.0f;
+        if (i < n) om = 1.0f - (1.0f - rn_exp_det(-sig[start + i] * dl[start + i]));
+        const int cnt = min(RN_WAVE, n - base);
+        for (int j = 0; j < cnt; ++j) {
+            t = t * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(om), j));
+            if (t <= thr) return base + j;
+        }
+    }
+    return n;
+}

@@ -103,18 +103,21 @@ k_nerf_loss(int64_t B, int K, const float* __restrict__ rgb, const float* __rest
 // half_out (optional): f16 copy of p[0, n_half) written in the same pass.
 __global__ void __launch_bounds__(256)
 k_adam(int64_t n, float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
-       float* __restrict__ v, float lr, float b1, float b2, float eps, float bc1, float bc2,
-       float grad_scale, _Float16* __restrict__ half_out, int64_t n_half) {
+       float* __restrict__ v, float step_size, float omb1, float b2, float omb2, float eps,
+       float bc2_sqrt, float grad_scale, _Float16* __restrict__ half_out, int64_t n_half) {
+    // torch.optim.Adam (single-tensor form): exp_avg.lerp_(g, 1-b1);
+    // exp_avg_sq.mul_(b2).addcmul_(g, g, 1-b2);
+    // p.addcdiv_(exp_avg, exp_avg_sq.sqrt() / sqrt(bc2) + eps, -lr/bc1)
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const float gi = g[i] * grad_scale;
         const float m0 = m[i];
-        const float mi = m0 + (1.0f - b1) * (gi - m0);
-        const float vi = v[i] * b2 + (1.0f - b2) * (gi * gi);
+        const float mi = m0 + omb1 * (gi - m0);
+        const float vi = v[i] * b2 + omb2 * (gi * gi);
         m[i] = mi;
         v[i] = vi;
-        const float denom = sqrtf(vi) / sqrtf(bc2) + eps;
-        const float pi = p[i] - (lr / bc1) * (mi / denom);
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        const float pi = p[i] - step_size * (mi / denom);
         p[i] = pi;
         if (i < n_half) half_out[i] = (_Float16)pi;
     }
@@ -168,19 +171,22 @@ int rn_nerf_loss(const float* rgb, const float* target_rgb, const float* opacity
 }
 
 int rn_adam(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
-            float lr, float beta1, float beta2, float eps, int32_t step, float grad_scale,
+            double lr, double beta1, double beta2, double eps, int32_t step, float grad_scale,
             void* params_f16, int64_t n_f16, void* stream) {
     RN_CHECK_ARG(n >= 0 && step >= 1 && n_f16 >= 0 && n_f16 <= n, "bad sizes");
     if (n == 0) return 0;
     RN_CHECK_ARG(params && grads && exp_avg && exp_avg_sq && (n_f16 == 0 || params_f16),
                  "null pointer");
-    const float bc1 = 1.0f - powf(beta1, (float)step);
-    const float bc2 = 1.0f - powf(beta2, (float)step);
+    // step constants in double, as torch / apex compute them on the host,
+    // rounded once to the kernel's fp32
+    const double bc1 = 1.0 - pow(beta1, (double)step);
+    const double bc2 = 1.0 - pow(beta2, (double)step);
     const int64_t nb = nblk(n, 256);
     const int blocks = (int)(nb < 256 * 16 ? nb : 256 * 16);
-    k_adam<<<blocks, 256, 0, (hipStream_t)stream>>>(n, params, grads, exp_avg, exp_avg_sq, lr,
-                                                    beta1, beta2, eps, bc1, bc2, grad_scale,
-                                                    (_Float16*)params_f16, n_f16);
+    k_adam<<<blocks, 256, 0, (hipStream_t)stream>>>(
+        n, params, grads, exp_avg, exp_avg_sq, (float)(lr / bc1), (float)(1.0 - beta1),
+        (float)beta2, (float)(1.0 - beta2), (float)eps, (float)sqrt(bc2), grad_scale,
+        (_Float16*)params_f16, n_f16);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -16,6 +16,7 @@ P = ctypes.c_void_p
 I32 = ctypes.c_int32
 I64 = ctypes.c_int64
 F32 = ctypes.c_float
+F64 = ctypes.c_double
 
 # name -> argtypes (all return int status).  Keep in sync with include/radnerf.h
 SIGNATURES = {
@@ -54,7 +55,7 @@ SIGNATURES = {
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],
-    "rn_adam": [P, P, P, P, I64, F32, F32, F32, F32, I32, F32, P, I64, P],
+    "rn_adam": [P, P, P, P, I64, F64, F64, F64, F64, I32, F32, P, I64, P],
     "rn_get_rays": [P, P, P, P, I64, P, P, P, P, P],
     "rn_pack_f16": [P, I64, P, I64, I32, I64, P, P],
     "rn_to_f16": [P, I64, P, P],

@@ -13,6 +13,8 @@ so sample counts never have to be read back; every kernel consumes the
 device-side counts.  Outputs equal the unfused drop-in path (rendering.py)
 for the same noise (tests/test_gpu_parity.py).
 """
+import collections
+
 import torch
 
 from . import layout as LY
@@ -64,6 +66,7 @@ class Workspace:
         self.queue = torch.zeros(3, **i)
         self._bwd_scratch = None
         self._chunks = None
+        self.generation = 0         # forwards run through this workspace (_MLRenderFn)
 
     def chunk_list(self, max_chunk, min_chunk, head_chunks=0):
         """rn_bwd_plan's chunk list, sized for the workspace capacity."""
@@ -413,6 +416,11 @@ class _MLRenderFn(torch.autograd.Function):
                 noise, bg, T_threshold, esf):
         rgb, opacity, depth, gate, imp = renderer.forward(rays_o, rays_d, gate_in2, noise, bg,
                                                           T_threshold, esf)
+        # the backward reads this step's samples from the renderer's workspace:
+        # stamp it, so a second forward through the same workspace before this
+        # backward is caught instead of silently differentiating the wrong step
+        renderer.ws.generation += 1
+        ctx.generation = renderer.ws.generation
         ctx.renderer = renderer
         ctx.save_for_backward(rays_o, rays_d, gate_in2, gate, bg)
         ctx.T = T_threshold
@@ -421,6 +429,11 @@ class _MLRenderFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, d_rgb, d_op, d_depth, d_gate):
         rays_o, rays_d, gate_in2, gate, bg = ctx.saved_tensors
+        if ctx.renderer.ws.generation != ctx.generation:
+            raise RuntimeError(
+                "ml_render_fused: the renderer's workspace was reused by another forward "
+                "(same model, gate and batch size) before this backward; run the backward "
+                "first, or render the other batch under torch.no_grad()")
         B, K = gate.shape
         dev = rays_o.device
         z = lambda *s: torch.zeros(*s, device=dev)
@@ -433,16 +446,30 @@ class _MLRenderFn(torch.autograd.Function):
         return gg, mg, ag, None, None, None, None, None, None, None, None
 
 
-_RENDERERS = {}
+_RENDERERS = collections.OrderedDict()
+MAX_RENDERERS = 4       # workspaces are ~0.3 GB per 1k rays x sub-NeRF: keep a few
 
 
-def get_renderer(model, gating_net, n_rays):
-    key = (id(model), id(gating_net), n_rays, str(model.mlp_params.device))
+def get_renderer(model, gating_net, n_rays, grad=True):
+    """The cached renderer (and workspace) of (model, gate, batch size).
+    Renders without autograd (grad=False) get their own workspace, so a
+    logging / validation render between a forward and its backward does not
+    overwrite the samples the backward reads.  Least recently used entries
+    beyond MAX_RENDERERS are dropped (their workspaces freed)."""
+    key = (id(model), id(gating_net), n_rays, str(model.mlp_params.device), bool(grad))
     r = _RENDERERS.get(key)
-    if r is None:
+    if r is None or r.model is not model or r.gate is not gating_net:
         r = FusedMLRenderer(model, gating_net, n_rays)
         _RENDERERS[key] = r
+    _RENDERERS.move_to_end(key)
+    while len(_RENDERERS) > MAX_RENDERERS:
+        _RENDERERS.popitem(last=False)
     return r
+
+
+def release_renderers():
+    """Drop every cached renderer and its device workspace."""
+    _RENDERERS.clear()
 
 
 def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):
@@ -460,7 +487,7 @@ def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **k
         bg = torch.rand(3, device=dev)
     else:
         bg = torch.zeros(3, device=dev)
-    r = get_renderer(model, gating_net, B)
+    r = get_renderer(model, gating_net, B, grad=torch.is_grad_enabled())
     rgb, opacity, depth, gate = _MLRenderFn.apply(
         model.xyz_encoder.params, model.mlp_params, gating_net.params, r, rays_o, rays_d, second,
         noise.contiguous(), bg, float(kwargs.get("T_threshold", 1e-4)), esf)

@@ -112,9 +112,11 @@ class _FieldFn(torch.autograd.Function):
         sigma = torch.empty(n, device=dev)
         rgb = torch.empty(n, 3, device=dev)
         # encoding cache for the backward (64 B/sample): only when a gradient
-        # will be asked for (density-grid updates run without)
+        # will be asked for.  needs_input_grad reflects the parameters'
+        # requires_grad even under no_grad, so the grad mode is checked too
+        # (density-grid updates run under no_grad and skip the cache)
         feat = None
-        if n > 0 and (ctx.needs_input_grad[2] or ctx.needs_input_grad[3]):
+        if n > 0 and torch.is_grad_enabled() and any(ctx.needs_input_grad[:4]):
             feat = torch.empty((n + 31) // 32 * 32, 32, device=dev, dtype=torch.float16)
         if n > 0:
             model._launch_field(True, xyzs, dirs, ind, sigma=sigma, rgb=rgb, feat=feat)

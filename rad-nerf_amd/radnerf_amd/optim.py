@@ -12,7 +12,9 @@ from ._lib import lib
 
 
 class FusedAdam(torch.optim.Optimizer):
-    def __init__(self, params, lr=1e-2, betas=(0.9, 0.99), eps=1e-15, weight_decay=0.0):
+    # defaults as apex.FusedAdam / torch.optim.Adam: train_ml.py:143 passes
+    # only lr and eps, so the reference runs betas (0.9, 0.999)
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-15, weight_decay=0.0):
         if weight_decay != 0.0:
             raise NotImplementedError("weight decay: train_ml.py uses none")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))

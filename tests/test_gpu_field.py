@@ -6,7 +6,7 @@ activations to f16 exactly where the oracle does (tcnn semantics), so the
 residual differences are fp32 summation order, occasionally flipping one f16
 ulp of an activation.  Tolerances (written per assertion):
   forward sigma, rgb:   |diff| <= 5e-3 + 1e-2*|ref|, and 99th pct <= 1e-3-level
-  backward grads:       ||g - g_ref|| / ||g_ref|| <= 2e-2 (f16 backward chain)
+  backward grads:       relative L2 per grid level / MLP layer (tests/parity.py)
 """
 import numpy as np
 import pytest
@@ -16,6 +16,10 @@ from oracle import field_oracle as fo
 from radnerf_amd import layout as LY
 from radnerf_amd import synthetic as S
 from radnerf_amd.networks import MNGP, Ray_Gate
+from parity import check_grads
+
+FIELD_GRID_TOL = 1e-3     # measured <= 3.8e-4
+FIELD_MLP_TOL = 1e-3      # measured <= 3.6e-4
 
 pytestmark = pytest.mark.gpu
 
@@ -86,13 +90,11 @@ def test_field_backward(cuda, zero_span):
     torch.autograd.backward([osig, orgb], [torch.from_numpy(ds), torch.from_numpy(dr)])
     g_grid = m.xyz_encoder.params.grad.cpu().view(-1, 2).numpy()
     g_mlp = m.mlp_params.grad.cpu().numpy()
-    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
-    assert rel(g_grid, gp.grad.numpy()) <= 2e-2, rel(g_grid, gp.grad.numpy())
-    assert rel(g_mlp[ind], mp.grad[ind].numpy()) <= 2e-2, rel(g_mlp[ind], mp.grad[ind].numpy())
+    # random points with N(0, 1) seeds: the f16 chain's relative error is
+    # larger than on rendered samples (no composite weighting)
+    check_grads(scale, g_grid, gp.grad.numpy(), g_mlp[ind], mp.grad[ind].numpy(),
+                tag=f"field zero_span={zero_span}", grid_tol=FIELD_GRID_TOL, mlp_tol=FIELD_MLP_TOL)
     assert np.abs(g_mlp[1 - ind]).max() == 0
-    for name, sl in LY.split_field_params(np.arange(LY.FIELD_PARAMS)).items():
-        idx = sl.reshape(-1)
-        assert rel(g_mlp[ind][idx], mp.grad[ind].numpy()[idx]) <= 3e-2, name
 
 
 @pytest.mark.parametrize("K", [2, 4, 8])
@@ -107,11 +109,15 @@ def test_gate_forward_backward(cuda, K):
     from oracle.ml_oracle import _split_gate
     gp = g.params.detach().cpu().clone().requires_grad_(True)
     ogate = fo.gate_forward(torch.from_numpy(x), _split_gate(gp, K))
-    assert np.abs(gate.detach().cpu().numpy() - ogate.detach().numpy()).max() <= 2e-3
+    e_gate = np.abs(gate.detach().cpu().numpy() - ogate.detach().numpy()).max()
+    print(f"gate K={K}: L_inf {e_gate:.2e}")
+    assert e_gate <= 1e-5      # split-precision activations: ~fp32 (gate.hip gate_split)
     assert np.allclose(gate.sum(1).detach().cpu().numpy(), 1, atol=1e-5)
     rng = np.random.default_rng(1)
     dg = rng.normal(0, 1, (3000, K)).astype(np.float32)
     gate.backward(torch.from_numpy(dg).to(cuda))
     ogate.backward(torch.from_numpy(dg))
     a, b = g.params.grad.cpu().numpy(), gp.grad.numpy()
-    assert np.linalg.norm(a - b) / np.linalg.norm(b) <= 2e-2
+    e = np.linalg.norm(a - b) / np.linalg.norm(b)
+    print(f"gate K={K}: grad rel {e:.2e}")
+    assert e <= 1.5e-3        # measured <= 5.2e-4

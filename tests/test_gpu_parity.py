@@ -145,9 +145,10 @@ def test_composite_train_fw_bw(cuda):
     assert np.abs(op.cpu().numpy() - oop).max() <= RGB_TOL
     assert np.abs(de.cpu().numpy() - ode).max() <= RGB_TOL
     assert np.abs(ws.cpu().numpy() - ows).max() <= 1e-5
-    # termination index may move by one only when T sits within rounding of T_threshold
-    assert np.abs(tot.cpu().numpy() - otot).max() <= 1
-    assert (tot.cpu().numpy() == otot).mean() > 0.99
+    # transmittance folds in the reference's serial order with the exponent
+    # shared with the oracle (rn_exp_det / det_expf): termination is bit-exact
+    assert np.array_equal(tot.cpu().numpy(), otot)
+    assert np.array_equal(ws.cpu().numpy() == 0, ows == 0)
     rng = np.random.default_rng(3)
     gO, gD = rng.normal(0, 1, n).astype(np.float32), rng.normal(0, 1, n).astype(np.float32)
     gR = rng.normal(0, 1, (n, 3)).astype(np.float32)
@@ -180,6 +181,7 @@ def test_composite_test_fw(cuda):
                            g_de, g_rgb)
     oracle.composite_test_fw(sig, rgbs, deltas, ts, alive, 1e-4, n_eff, op, de, rgb)
     assert np.array_equal(g_alive.cpu().numpy(), alive)
+    assert (alive == -1).sum() > 50            # enough rays terminate to exercise the break
     assert np.abs(g_op.cpu().numpy() - op).max() <= RGB_TOL
     assert np.abs(g_rgb.cpu().numpy() - rgb).max() <= RGB_TOL
     assert np.abs(g_de.cpu().numpy() - de).max() <= RGB_TOL
@@ -196,3 +198,57 @@ def test_morton_packbits(cuda):
     bits = torch.zeros(2 * 128 ** 3 // 8, dtype=torch.uint8, device=cuda)
     vren.packbits(_t(grid, cuda), 0.3, bits)
     assert np.array_equal(bits.cpu().numpy(), oracle.packbits(grid, 0.3))
+
+
+def test_composite_termination_at_threshold(cuda):
+    """Segments built so the serial transmittance lands within a few ulps of
+    T_threshold at a chosen sample (both sides): the tree-order product cannot
+    decide these, the serial fallback must, and the break (total_samples and
+    the samples that get weights / gradients) equals the oracle's."""
+    rng = np.random.default_rng(7)
+    thr = np.float32(1e-4)
+    n_seg = 240
+    sig_l, dl_l, counts = [], [], []
+    for i in range(n_seg):
+        k = int(rng.integers(0, 400))
+        n = k + int(rng.integers(1, 40))
+        dl = (np.float32(np.sqrt(3) / 1024) * rng.uniform(0.5, 2, n)).astype(np.float32)
+        # samples before k leave T well above thr: total optical depth ~ 7
+        sig = (rng.uniform(0.2, 1.8, n) * 7.0 / max(1, k) / dl).astype(np.float32)
+        sig[k + 1:] = rng.uniform(0, 50, n - k - 1).astype(np.float32)
+        # serial T before sample k, with the shared exponent
+        E = oracle.det_expf(-sig[:k] * dl[:k])
+        T = np.float32(1.0)
+        for e in E:
+            T = np.float32(T * np.float32(np.float32(1.0) - np.float32(np.float32(1.0) - e)))
+        if T <= thr:
+            continue
+        Ek = np.float64(thr) / np.float64(T)
+        s = np.float32(-np.log(Ek) / np.float64(dl[k]))
+        sig[k] = np.float32(s) + np.float32(np.spacing(s)) * np.float32(rng.integers(-4, 5))
+        sig_l.append(sig); dl_l.append(dl); counts.append(n)
+    counts = np.array(counts, np.int64)
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    sig = np.concatenate(sig_l).astype(np.float32)
+    dl = np.concatenate(dl_l).astype(np.float32)
+    N = len(sig)
+    rgbs = rng.random((N, 3), dtype=np.float32)
+    ts = np.cumsum(dl).astype(np.float32)
+    rays_a = np.stack([np.arange(len(counts)), starts, counts], 1).astype(np.int64)
+    g = lambda a: _t(a, cuda)
+    tot, op, de, rgb, ws = vren.composite_train_fw(g(sig), g(rgbs), g(dl), g(ts), g(rays_a), 1e-4)
+    otot, oop, ode, orgb, ows = oracle.composite_train_fw(sig, rgbs, dl, ts, rays_a, 1e-4)
+    assert np.array_equal(tot.cpu().numpy(), otot)
+    assert (otot < counts).sum() > len(counts) // 4        # many break at the threshold sample
+    assert np.array_equal(ws.cpu().numpy() == 0, ows == 0)
+    assert np.abs(rgb.cpu().numpy() - orgb).max() <= RGB_TOL
+    gO = rng.normal(0, 1, len(counts)).astype(np.float32)
+    gD = rng.normal(0, 1, len(counts)).astype(np.float32)
+    gR = rng.normal(0, 1, (len(counts), 3)).astype(np.float32)
+    gW = np.zeros(N, np.float32)
+    dsig, drgb = vren.composite_train_bw(g(gO), g(gD), g(gR), g(gW), g(sig), g(rgbs), ws, g(dl),
+                                         g(ts), g(rays_a), op, de, rgb, 1e-4)
+    odsig, odrgb = oracle.composite_train_bw(gO, gD, gR, gW, sig, rgbs, ows, dl, ts, rays_a,
+                                             oop, ode, orgb, 1e-4)
+    assert np.array_equal(drgb.cpu().numpy() == 0, odrgb == 0)
+    assert np.abs(drgb.cpu().numpy() - odrgb).max() <= 1e-4

@@ -23,6 +23,7 @@ from radnerf_amd import layout as LY
 from radnerf_amd import synthetic as S
 from radnerf_amd.networks import MNGP, NGP, Ray_Gate
 from radnerf_amd.rendering import ml_render, render
+from parity import check_grads
 
 pytestmark = pytest.mark.gpu
 
@@ -60,9 +61,8 @@ def test_ngp_render_train_vs_oracle(cuda):
     e_op = np.abs(res["opacity"].detach().cpu().numpy() - ref["opacity"]).max()
     e_de = np.abs(res["depth"].detach().cpu().numpy() - ref["depth"][:, 0]).max()
     assert e_rgb <= 1e-4 and e_op <= 1e-4 and e_de <= 1e-4, (e_rgb, e_op, e_de)
-    rel = lambda a, b: np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
-    assert rel(m.xyz_encoder.params.grad.cpu().view(-1, 2).numpy(), ref["grid_grad"]) <= 5e-2
-    assert rel(m.mlp_params.grad.cpu().numpy(), ref["mlp_grad"]) <= 5e-2
+    check_grads(scale, m.xyz_encoder.params.grad.cpu().view(-1, 2).numpy(), ref["grid_grad"],
+                m.mlp_params.grad.cpu().numpy(), ref["mlp_grad"], tag="NGP render")
 
 
 @pytest.mark.parametrize("K", [1, 2])
@@ -117,7 +117,9 @@ def test_density_grid_update(cuda):
         expect = np.maximum(0.5 * 0.95, sig.detach().numpy())
         got = grid[0, idx[sel]]
         assert np.allclose(got, expect, rtol=1e-2, atol=1e-6)
-        # bitfield == packbits(grid > min(mean, thr)) in Morton byte order
-        mean = grid[grid > 0].mean()
+        # bitfield == packbits(grid > min(mean, thr)) in Morton byte order; the
+        # mean is the reference's torch reduction (networks.py:405) on the device
+        dg = getattr(m, f"density_grid_{i}")
+        mean = dg[dg > 0].mean().item()
         bits = oracle.packbits(grid.reshape(-1), min(float(mean), thr))
         assert np.array_equal(getattr(m, f"density_bitfield_{i}").cpu().numpy(), bits)

@@ -56,14 +56,19 @@ def test_fused_loss_matches_reference_formula(cuda, K):
     assert close(d_gate, leaves["gating_code"].grad)
 
 
-def test_fused_adam_matches_torch_adam(cuda):
+@pytest.mark.parametrize("betas", [(0.9, 0.99), None])
+def test_fused_adam_matches_torch_adam(cuda, betas):
+    """betas=None: constructed as train_ml.py:143 constructs apex.FusedAdam
+    (lr and eps only), against torch.optim.Adam's defaults (0.9, 0.999)."""
     g = torch.Generator().manual_seed(3)
     p0 = torch.randn(100_003, generator=g)
     grads = [torch.randn(100_003, generator=g) * 1e-2 for _ in range(5)]
     ref = torch.nn.Parameter(p0.clone())
-    opt_ref = torch.optim.Adam([ref], lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    kw = {} if betas is None else {"betas": betas}
+    opt_ref = torch.optim.Adam([ref], lr=1e-2, eps=1e-15, **kw)
     ours = torch.nn.Parameter(p0.clone().to(cuda))
-    opt = FusedAdam([ours], lr=1e-2, betas=(0.9, 0.99), eps=1e-15)
+    opt = FusedAdam([ours], lr=1e-2, eps=1e-15, **kw)
+    assert opt.defaults["betas"] == opt_ref.defaults["betas"]
     for gr in grads:
         ref.grad = gr.clone()
         opt_ref.step()
@@ -88,22 +93,26 @@ def _setup(cuda, B, K, scale=0.5):
     return m.to(cuda), g.to(cuda)
 
 
-def test_fused_train_step_matches_autograd(cuda):
-    B, K = 512, 2
-    m, g = _setup(cuda, B, K)
-    o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, 0.5))
+@pytest.mark.parametrize("B,K,scale", [(512, 2, 0.5), (512, 4, 16.0)])
+def test_fused_train_step_matches_autograd(cuda, B, K, scale):
+    """(512, 4, 16): config C4's branch -- K = 4 with depth-mutual, exp step
+    1/256, 6 cascades, black background (scripts/rad_360v2.sh:3-7)."""
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g = _setup(cuda, B, K, scale)
+    o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, scale))
     nz = torch.from_numpy(S.noise(K, B)).to(cuda)
     tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(5)).to(cuda)
     # reference structure: render (autograd) -> NeRFLoss -> sum of means -> backward
     m.zero_grad(); g.zero_grad()
-    res = ml_render_fused(m, g, o, d, d, noise=nz)
+    res = ml_render_fused(m, g, o, d, d, noise=nz, exp_step_factor=esf)
     ld = NeRFLoss()(res, {"rgb": tgt}, **LAMBDAS)
+    assert "depth_mutual" in ld or K == 1
     sum(v.mean() for v in ld.values()).backward()
     ref = [m.xyz_encoder.params.grad.clone(), m.mlp_params.grad.clone(), g.params.grad.clone()]
     # fused train step
     r = get_renderer(m, g, B)
-    bg = torch.ones(3, device=cuda)
-    terms, grads = r.train_step(o, d, d, tgt, nz, bg, **LAMBDAS)
+    bg = torch.ones(3, device=cuda) if esf == 0 else torch.zeros(3, device=cuda)
+    terms, grads = r.train_step(o, d, d, tgt, nz, bg, exp_step_factor=esf, **LAMBDAS)
     for k in ld:
         assert abs(float(terms[k]) - float(ld[k].mean().detach())) <= 1e-5 * max(1.0, abs(float(ld[k].mean().detach()))), k
     rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))

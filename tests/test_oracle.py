@@ -190,3 +190,34 @@ def test_multiscale_cascades_exp_step():
     assert dl.min() >= lo and dl.max() <= hi
     exp = np.clip(ts * np.float32(1 / 256), lo, hi)
     assert np.array_equal(dl, exp.astype(np.float32))
+
+
+def test_det_expf_accuracy():
+    """The compositing exponent shared by the oracle and the kernels
+    (det_expf / rn_exp_det, a fixed IEEE operation sequence in place of CUDA's
+    __expf) is within 1 ulp of exp over the compositing range."""
+    rng = np.random.default_rng(0)
+    x = np.concatenate([-rng.exponential(2.0, 20000), -rng.uniform(0, 87, 5000),
+                        [0.0, -1e-30, -1e-7, -0.5, -0.6931472, -1.0, -20.0, -86.9]]).astype(np.float32)
+    got = oracle.det_expf(x)
+    ref = np.exp(x.astype(np.float64))
+    ulp = np.spacing(np.float32(ref).astype(np.float32))
+    err = np.abs(got.astype(np.float64) - ref) / ulp
+    assert err.max() <= 1.0, err.max()
+    assert oracle.det_expf([0.0])[0] == 1.0 and oracle.det_expf([-100.0])[0] == 0.0
+
+
+def test_ml_march_threads_invariant(monkeypatch):
+    """The OpenMP oracle march (count, ray-order starts, write) equals its
+    sequential form: the totals and per-segment starts are the prefix sums."""
+    o, d = S.rays(300, 16.0, seed=4)
+    bits = S.bitfields(3, 6, p=0.3, seed=5)
+    nz = S.noise(3, 300, seed=6)
+    c = np.zeros(3, np.float32); h = np.full(3, 16.0, np.float32)
+    counts, starts, xyzs, ts, dl, total = oracle.ml_march(o, d, c, h, nz, bits, 6, 16.0, 1 / 256)
+    flat = counts.reshape(-1).astype(np.int64)
+    assert total == flat.sum()
+    assert np.array_equal(starts.reshape(-1), np.concatenate([[0], np.cumsum(flat)[:-1]]))
+    for g in range(0, len(flat), 37):
+        seg = ts[starts.reshape(-1)[g]:starts.reshape(-1)[g] + flat[g]]
+        assert np.all(np.diff(seg) > 0)
