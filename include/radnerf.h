@@ -62,6 +62,12 @@ int rn_raymarching_train_write(const float* rays_o, const float* rays_d, const f
 int rn_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, const float* ts,
                             const int64_t* rays_a, int64_t n_rows, float* dL_drays_o,
                             float* dL_drays_d, void* stream);
+/* the same for the fused (model-major, per (model, ray) segment) layout of
+ * rn_ml_compact: counts / offsets [K][B]; dL_drays_o / dL_drays_d (B, 3)
+ * written (sums over the K sub-NeRFs' samples of each ray).                 */
+int rn_ml_march_bw(const int32_t* counts, const int32_t* offsets, int64_t n_rays,
+                   int32_t n_models, const float* ts, const float* dL_dxyzs,
+                   const float* dL_ddirs, float* dL_drays_o, float* dL_drays_d, void* stream);
 
 /* exclusive scan of counts[n_seg][n_per]; segment k starts at an `align`
  * multiple: seg_base[k], seg_count[k]; meta[0] = aligned end, meta[1] = total.
@@ -262,9 +268,43 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
 int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
                 int32_t n_models, const void* frags, float* gate, float* importance,
                 int32_t n_blocks, void* stream);
+/* rn_gate_bwd: dL_dinput (optional, (B, 6) fp32, written): the gradient into
+ * the gate input cat(in0, in1), as tcnn's Network backward provides when the
+ * input requires grad (rays_o / rays_d under --optimize_ext,
+ * train_ml.py:90-93); needs dinput_frags (4 transposed W0 fragments,
+ * radnerf_amd/layout.py gate_dinput_frag_index).                            */
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
                 int32_t n_models, const void* frags, const float* dL_dgate, float* dw,
-                int32_t n_params, int32_t n_blocks, void* stream);
+                int32_t n_params, const void* dinput_frags, float* dL_dinput,
+                int32_t n_blocks, void* stream);
+
+/* ---- field input gradients and density-only evaluation (field_aux.hip) -----
+ * rn_field_dinput: dL/dxyz and dL/ddir (fp32, (N, 3) each, written, indexed
+ * like the samples) of MNGP.forward (models/networks.py:300-328: clip, hash
+ * grid, d/|d|, SH, MLPs) for the seeds dL_dsigma / dL_drgb -- what tcnn's
+ * Encoding / Network backward returns for inputs that require grad
+ * (--optimize_ext, train_ml.py:90-93; custom_functions.py:102-112 consumes
+ * it).  Same sample modes and arguments as rn_field_fwd/_bwd, plus
+ * dinput_frags ([K][4][512] f16: the rgb net's SH columns transposed,
+ * radnerf_amd/layout.py field_dinput_frag_index) and the optional encoding
+ * cache of the forward.
+ * rn_field_density: MNGP.density(x, ind, return_feat) (networks.py:291-309):
+ * hash grid + geo MLP of one sub-NeRF (frags of that model); sigma (N) and,
+ * if geo_feat is not NULL, h[:, 1:17] (N, 16) fp32 of the f16 values.       */
+int rn_field_dinput(const float* xyzs, const float* dirs, int64_t n_samples, const float* ts,
+                    const int32_t* ray_of, const float* rays_o, const float* rays_d,
+                    const int32_t* seg_base, const int32_t* seg_count, int32_t n_models,
+                    const void* grid_f16, const uint32_t* level_offset,
+                    const uint32_t* level_hsize, const uint32_t* level_res,
+                    const float* level_scale, const float* xyz_min, const float* extent,
+                    const void* frags, const void* dinput_frags, const float* dL_dsigma,
+                    const float* dL_drgb, const void* feat_cache, float* dL_dxyz,
+                    float* dL_ddir, int32_t blocks_per_model, void* stream);
+int rn_field_density(const float* xyzs, int64_t n_samples, const void* grid_f16,
+                     const uint32_t* level_offset, const uint32_t* level_hsize,
+                     const uint32_t* level_res, const float* level_scale, const float* xyz_min,
+                     const float* extent, const void* frags, float* sigma, float* geo_feat,
+                     void* stream);
 
 /* ---- training-step epilogue ---------------------
  * rn_nerf_loss: losses.py:44-76 (NeRFLoss: rgb MSE, opacity entropy, CV^2 of

@@ -169,6 +169,17 @@ def field_forward(x, d, grid_params, mlp, lv, xyz_min, xyz_max):
     return sigma, rgb
 
 
+def density_forward(x, grid_params, mlp, lv, xyz_min, xyz_max):
+    """MNGP.density(x, ind, return_feat=True) (networks.py:291-309): sigma (N)
+    and the geo features h[:, 1:17] (f16 values) of one sub-NeRF."""
+    u = unit_coords(x, xyz_min, xyz_max)
+    e = r16(hash_encode(u, grid_params, lv))
+    W = {k: r16(v) for k, v in mlp.items()}
+    h1 = r16(torch.relu(e @ W["g1"].t()))
+    g32 = h1 @ W["g2"].t()
+    return TruncExp.apply(g32[:, 0]), r16(g32)[:, 1:]
+
+
 def gate_forward(x6, gate_w):
     """Ray_Gate.forward: softmax(MLP(x6)) with f16 input and weights (tcnn) and
     fp32 hidden activations / logits.  tcnn rounds those to f16; at scale 16

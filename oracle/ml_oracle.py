@@ -36,8 +36,16 @@ def _split_gate(flat, K):
 
 
 def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gate_master,
-                  scale, seeds=None, bg=None, T_threshold=1e-4, log2_T=19, grid_size=128):
+                  scale, seeds=None, bg=None, T_threshold=1e-4, log2_T=19, grid_size=128,
+                  input_grads=False):
     """One fwd (+ bwd if seeds) step.  All inputs numpy / CPU tensors.
+
+    input_grads: also differentiate w.r.t. rays_o / rays_d (--optimize_ext,
+    train_ml.py:90-93): through the gate input, the field's positions and
+    directions (autograd over the field restatement) and RayMarcher.backward
+    (custom_functions.py:102-112: per-ray sums of dL/dxyz and dL/dxyz * t +
+    dL/ddir).  Adds "drays_o", "drays_d" (B, 3) and per-sample "dxyzs",
+    "ddirs" lists (one per sub-NeRF) to the result.
 
     grid_master (E,2) fp32, mlp_master (K,9472) fp32, gate_master (12672+64K,)
     fp32.  seeds = (dL_drgb (B,3), dL_dopacity (B), dL_ddepth (B,K)).
@@ -55,8 +63,8 @@ def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gat
     center = np.zeros(3, np.float32)
     half = np.full(3, scale, np.float32)
 
-    o_t = torch.from_numpy(np.asarray(rays_o, np.float32))
-    d_t = torch.from_numpy(np.asarray(rays_d, np.float32))
+    o_t = torch.from_numpy(np.asarray(rays_o, np.float32).copy()).requires_grad_(input_grads)
+    d_t = torch.from_numpy(np.asarray(rays_d, np.float32).copy()).requires_grad_(input_grads)
     grid_p = torch.tensor(np.asarray(grid_master, np.float32)).half().float().requires_grad_(True)
     mlp_p = torch.tensor(np.asarray(mlp_master, np.float32)).requires_grad_(True)
     gate_p = torch.tensor(np.asarray(gate_master, np.float32)).requires_grad_(True)
@@ -70,18 +78,18 @@ def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gat
     res = {"counts": counts, "starts": starts, "xyzs": xyzs, "ts": ts, "deltas": deltas,
            "total": total, "gate": gate.detach().numpy(), "ray_of": ray_of}
 
-    sig_l, rgb_l, Ok, Dk, RGBk, ws_l, used_l, ra_l = [], [], [], [], [], [], [], []
+    sig_l, rgb_l, Ok, Dk, RGBk, ws_l, used_l, ra_l, x_l = [], [], [], [], [], [], [], [], []
     for k in range(K):
         base = int(starts[k, 0]) if B > 0 else 0
         n_k = int(counts[k].sum())
         sl = slice(base, base + n_k)
-        x = torch.from_numpy(xyzs[sl])
+        x = torch.from_numpy(xyzs[sl].copy()).requires_grad_(input_grads)
         d = d_t[torch.from_numpy(ray_of[sl])]
         sigma, rgb = fo.field_forward(x, d, grid_p, _split_field(mlp_p[k]), lv, xyz_min, xyz_max)
         rays_a = np.stack([np.arange(B), starts[k] - base, counts[k]], 1).astype(np.int64)
         total_k, O, D, RGB, ws = oracle.composite_train_fw(
             sigma.detach().numpy(), rgb.detach().numpy(), deltas[sl], ts[sl], rays_a, T_threshold)
-        sig_l.append(sigma); rgb_l.append(rgb); ra_l.append(rays_a)
+        sig_l.append(sigma); rgb_l.append(rgb); ra_l.append(rays_a); x_l.append(x)
         Ok.append(O); Dk.append(D); RGBk.append(RGB); ws_l.append(ws); used_l.append(total_k)
 
     O_t = torch.tensor(np.stack(Ok), requires_grad=True)       # (K,B)
@@ -118,6 +126,20 @@ def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gat
         if n_k:
             torch.autograd.backward([sig_l[k], rgb_l[k]],
                                     [torch.from_numpy(dsig), torch.from_numpy(drgb)])
+    if input_grads:
+        # RayMarcher.backward: segment sums over each ray's samples (fp64)
+        go = np.zeros((B, 3)) if o_t.grad is None else o_t.grad.numpy().astype(np.float64)
+        gd = np.zeros((B, 3)) if d_t.grad is None else d_t.grad.numpy().astype(np.float64)
+        dx_l = []
+        for k in range(K):
+            base = int(starts[k, 0]) if B > 0 else 0
+            n_k = int(counts[k].sum())
+            gx = np.zeros((n_k, 3)) if x_l[k].grad is None else x_l[k].grad.numpy().astype(np.float64)
+            rk = ray_of[base:base + n_k]
+            np.add.at(go, rk, gx)
+            np.add.at(gd, rk, gx * ts[base:base + n_k, None].astype(np.float64))
+            dx_l.append(gx)
+        res.update({"drays_o": go, "drays_d": gd, "dxyzs": dx_l})
     res.update({"dsigmas": dsig_l, "drgbs": drgb_l,
                 "grid_grad": grid_p.grad.numpy() if grid_p.grad is not None else None,
                 "mlp_grad": mlp_p.grad.numpy() if mlp_p.grad is not None else None,

@@ -24,6 +24,8 @@ struct GateArgs {
     const float* dgate;                          // (B,K) dL/dgate
     float* dw;                                   // (n_params)
     int n_params;
+    const rn_half* dfrags;                       // [4][512] W0^T (input gradient), or null
+    float* dx;                                   // (B,6) dL/dinput, or null
 };
 
 namespace {
@@ -247,6 +249,20 @@ k_gate_bwd(GateArgs a) {
             rn_acc_to_frags_masked(b0, st.h[L - 1][0], st.h[L - 1][1], dh[L - 1][0], dh[L - 1][1]);
             rn_acc_to_frags_masked(b1, st.h[L - 1][2], st.h[L - 1][3], dh[L - 1][2], dh[L - 1][3]);
         }
+        // input gradient (tcnn Network backward into its input, when the rays
+        // require grad): dX = W0^T dH0, rows 0..5 = (in0, in1)
+        if (a.dx) {
+            f32x16 b = rn_zero16();
+#pragma unroll
+            for (int q = 0; q < 4; ++q) b = rn_mfma(rn_frag(a.dfrags, q), dh[0][q], b);
+            if (valid) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int row = (i & 3) + 8 * (i >> 2) + 4 * h;
+                    if (row < 6) a.dx[r * 6 + row] = b[i] * ginv;
+                }
+            }
+        }
         // W4: dY = dz (features 0..15, 16..31 zero), X = H3
         rn_img_write(imgY, 0, dz0); rn_img_write(imgY, 1, z8);
 #pragma unroll
@@ -308,7 +324,7 @@ int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
 
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays, int32_t n_models,
                 const void* frags, const float* dL_dgate, float* dw, int32_t n_params,
-                int32_t n_blocks, void* stream) {
+                const void* dinput_frags, float* dL_dinput, int32_t n_blocks, void* stream) {
     RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && n_models <= 16 && n_blocks >= 1, "bad sizes");
     RN_CHECK_ARG(n_params == 12672 + 64 * n_models, "n_params mismatch");
     if (n_rays == 0) return 0;
@@ -318,6 +334,8 @@ int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
     a.in0 = in0; a.in1 = in1; a.stride = stride; a.n_rays = n_rays; a.K = n_models;
     a.frags = (const rn_half*)frags; a.dgate = dL_dgate; a.dw = dw;
     a.n_params = n_params;
+    RN_CHECK_ARG(!dL_dinput || dinput_frags, "the input gradient needs dinput_frags");
+    a.dfrags = (const rn_half*)dinput_frags; a.dx = dL_dinput;
     k_gate_bwd<<<n_blocks, GATE_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     RN_CHECK_LAUNCH();
     return 0;

@@ -580,6 +580,39 @@ k_march_train_bw(int n_rows, const float* __restrict__ gx, const float* __restri
     }
 }
 
+// RayMarcher.backward (custom_functions.py:102-112) for the fused layout: per
+// ray, over the K sub-NeRFs' (t, ray) segments, dL/drays_o = sum dL/dxyz and
+// dL/drays_d = sum (dL/dxyz t + dL/ddir); sample positions are fmaf(t, d, o).
+// Wave per ray, fixed summation order (deterministic).
+__global__ void __launch_bounds__(256)
+k_ml_march_bw(int n_rays, int K, const int32_t* __restrict__ counts,
+              const int32_t* __restrict__ offsets, const float* __restrict__ ts,
+              const float* __restrict__ gx, const float* __restrict__ gd,
+              float* __restrict__ go, float* __restrict__ gdir) {
+    const int r = blockIdx.x * (blockDim.x / RN_WAVE) + (threadIdx.x / RN_WAVE);
+    if (r >= n_rays) return;
+    const int lane = rn_lane();
+    float o0 = 0.f, o1 = 0.f, o2 = 0.f, d0 = 0.f, d1 = 0.f, d2 = 0.f;
+    for (int k = 0; k < K; ++k) {
+        const int64_t start = offsets[(int64_t)k * n_rays + r];
+        const int n = counts[(int64_t)k * n_rays + r];
+        for (int i = lane; i < n; i += RN_WAVE) {
+            const int64_t s = start + i;
+            const float t = ts[s];
+            const float x0 = gx[3 * s], x1 = gx[3 * s + 1], x2 = gx[3 * s + 2];
+            o0 += x0; o1 += x1; o2 += x2;
+            d0 += fmaf(x0, t, gd[3 * s]); d1 += fmaf(x1, t, gd[3 * s + 1]);
+            d2 += fmaf(x2, t, gd[3 * s + 2]);
+        }
+    }
+    o0 = rn_wave_sum(o0); o1 = rn_wave_sum(o1); o2 = rn_wave_sum(o2);
+    d0 = rn_wave_sum(d0); d1 = rn_wave_sum(d1); d2 = rn_wave_sum(d2);
+    if (lane == 0) {
+        go[3 * r] = o0; go[3 * r + 1] = o1; go[3 * r + 2] = o2;
+        gdir[3 * r] = d0; gdir[3 * r + 1] = d1; gdir[3 * r + 2] = d2;
+    }
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -756,6 +789,19 @@ int rn_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, const 
                  "null pointer");
     k_march_train_bw<<<nblk(n_rows, 4), 256, 0, (hipStream_t)stream>>>(
         (int)n_rows, dL_dxyzs, dL_ddirs, ts, rays_a, dL_drays_o, dL_drays_d);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_ml_march_bw(const int32_t* counts, const int32_t* offsets, int64_t n_rays,
+                   int32_t n_models, const float* ts, const float* dL_dxyzs,
+                   const float* dL_ddirs, float* dL_drays_o, float* dL_drays_d, void* stream) {
+    RN_CHECK_ARG(n_rays >= 0 && n_models >= 1, "bad sizes");
+    if (n_rays == 0) return 0;
+    RN_CHECK_ARG(counts && offsets && ts && dL_dxyzs && dL_ddirs && dL_drays_o && dL_drays_d,
+                 "null pointer");
+    k_ml_march_bw<<<nblk(n_rays, 4), 256, 0, (hipStream_t)stream>>>(
+        (int)n_rays, n_models, counts, offsets, ts, dL_dxyzs, dL_ddirs, dL_drays_o, dL_drays_d);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -23,6 +23,10 @@ SIGNATURES = {
     "rn_ray_aabb_intersect": [P, P, P, P, I64, I64, I32, P, P, P, P],
     "rn_ray_sphere_intersect": [P, P, P, P, I64, I64, I32, P, P, P, P],
     "rn_raymarching_train_bw": [P, P, P, P, I64, P, P, P],
+    "rn_ml_march_bw": [P, P, I64, I32, P, P, P, P, P, P],
+    "rn_field_dinput": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                        P, I32, P],
+    "rn_field_density": [P, I64, P, P, P, P, P, P, P, P, P, P, P],
     "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "rn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
     "rn_raymarching_train_count": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P],
@@ -53,7 +57,7 @@ SIGNATURES = {
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,
                             P, P, I32, I32, P],
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
-    "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, I32, P],
+    "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, P, P, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],
     "rn_adam": [P, P, P, P, I64, F64, F64, F64, F64, I32, F32, P, I64, P],
     "rn_get_rays": [P, P, P, P, I64, P, P, P, P, P],

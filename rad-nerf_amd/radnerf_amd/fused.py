@@ -161,6 +161,9 @@ class FusedMLRenderer:
         # beside composite_bw, "main" in line before field_bwd
         self.gate_grad_here = True
         self.gate_bwd_at = "field"
+        # input gradients (dL/drays_o, dL/drays_d) in backward(): set by
+        # _MLRenderFn when the rays require grad (--optimize_ext)
+        self.input_grad = False
         # record HIP events around every launch (True) or the named ones (a set)
         self.trace = False
         self.events = {}
@@ -356,14 +359,18 @@ class FusedMLRenderer:
         side = self._side(dev)
         main = torch.cuda.current_stream(dev)
 
+        gate_dx = self._gate_dinput(B, dev) if self.input_grad else None
+        gate_dfr = g.packed_dinput_frags() if gate_dx is not None else None
+
         def gate_bwd(stream):
             frags = g.packed_frags()
             if stream is side:
                 side.wait_stream(main)
             self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
                      frags.data_ptr(), dgate.data_ptr(), gate_grad.data_ptr(),
-                     gate_grad.numel(), max(1, min(128, (B + 127) // 128)), stream.cuda_stream,
-                     stream=stream)
+                     gate_grad.numel(), None if gate_dfr is None else gate_dfr.data_ptr(),
+                     None if gate_dx is None else gate_dx.data_ptr(),
+                     max(1, min(128, (B + 127) // 128)), stream.cuda_stream, stream=stream)
 
         # gate backward: it only needs dL/dgate (combine_bw)
         gate_at = self.gate_bwd_at if self.gate_grad_here else None
@@ -383,10 +390,45 @@ class FusedMLRenderer:
         elif gate_at == "main":         # in line, before field_bwd
             gate_bwd(main)
         self._field(False, rays_o, rays_d, st, grid_grad, mlp_grad)
+        if self.input_grad:
+            self._input_grads(rays_o, rays_d, st)
         if gate_at in ("early", "field"):
             main.wait_stream(side)
             gate_grad.record_stream(side)
+            if gate_dx is not None:
+                gate_dx.record_stream(side)
         return grid_grad, mlp_grad, gate_grad
+
+    def _gate_dinput(self, B, dev):
+        w = self.ws
+        if getattr(w, "gate_dx", None) is None or w.gate_dx.shape[0] != B:
+            w.gate_dx = torch.empty(B, 6, device=dev)
+        return w.gate_dx
+
+    def _input_grads(self, rays_o, rays_d, st):
+        """dL/drays_o, dL/drays_d through the field and the march (the path
+        --optimize_ext differentiates, train_ml.py:90-93): rn_field_dinput over
+        the compact samples of all K sub-NeRFs, then rn_ml_march_bw sums each
+        ray's samples (custom_functions.py:102-112).  The gate's own input
+        gradient is in ws.gate_dx ((B, 6): rays_o | second gate input)."""
+        m, w, L = self.model, self.ws, lib()
+        if getattr(w, "dxyz", None) is None:
+            w.dxyz = torch.empty(w.capacity, 3, device=w.device)
+            w.ddir = torch.empty(w.capacity, 3, device=w.device)
+            w.drays_o = torch.empty(w.B, 3, device=w.device)
+            w.drays_d = torch.empty(w.B, 3, device=w.device)
+        lo, lh, lr, ls = m.xyz_encoder.level_ptrs()
+        self._ev("field_dinput", L.field_dinput, None, None, 0, w.ts.data_ptr(),
+                 w.ray_of.data_ptr(), rays_o.data_ptr(), rays_d.data_ptr(),
+                 w.seg_base.data_ptr(), w.seg_count.data_ptr(), m.size,
+                 m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
+                 m._h_ext.ctypes.data, m.packed_frags().data_ptr(),
+                 m.packed_dinput_frags().data_ptr(), w.dsigma.data_ptr(), w.drgb.data_ptr(),
+                 w.feat.data_ptr() if self.feat_cache else None, w.dxyz.data_ptr(),
+                 w.ddir.data_ptr(), self.fwd_blocks, st)
+        self._ev("march_bw", L.ml_march_bw, w.counts.data_ptr(), w.offsets.data_ptr(), w.B, m.size,
+                 w.ts.data_ptr(), w.dxyz.data_ptr(), w.ddir.data_ptr(), w.drays_o.data_ptr(),
+                 w.drays_d.data_ptr(), st)
 
     def _dgate(self, B, G):
         return self.ws.dgate
@@ -441,9 +483,21 @@ class _MLRenderFn(torch.autograd.Function):
         d_op = z(B) if d_op is None else d_op.float().contiguous()
         d_depth = None if d_depth is None else d_depth.float().contiguous()
         d_gate = None if d_gate is None else d_gate.float().contiguous()
-        gg, mg, ag = ctx.renderer.backward(rays_o, rays_d, gate_in2, gate, bg, d_rgb, d_op,
-                                           d_depth, d_gate, ctx.T)
-        return gg, mg, ag, None, None, None, None, None, None, None, None
+        r = ctx.renderer
+        need_o, need_d, need_2 = ctx.needs_input_grad[4:7]
+        r.input_grad = bool(need_o or need_d or need_2)
+        try:
+            gg, mg, ag = r.backward(rays_o, rays_d, gate_in2, gate, bg, d_rgb, d_op, d_depth,
+                                    d_gate, ctx.T)
+        finally:
+            input_grad, r.input_grad = r.input_grad, False
+        do = dd = d2 = None
+        if input_grad:
+            w = r.ws
+            do = w.drays_o + w.gate_dx[:, 0:3] if need_o else None
+            dd = w.drays_d.clone() if need_d else None
+            d2 = w.gate_dx[:, 3:6].contiguous() if need_2 else None
+        return gg, mg, ag, None, do, dd, d2, None, None, None, None
 
 
 _RENDERERS = collections.OrderedDict()

@@ -167,6 +167,23 @@ def field_frag_index():
     return np.concatenate(F)
 
 
+def field_dinput_frag_index():
+    """(4*512,) int32: the rgb net's SH columns transposed, Wr1[:, 0:16]^T as A
+    fragments (rows = SH inputs 0..15, k = the 64 rgb hidden units in 4
+    steps): dL/dSH = Wr1_sh^T dL/dR1 for the input gradient (rn_field_dinput)."""
+    F = [_frag(lambda r, h, j, q=q: _w("r1", _kin(q, h, j), r) if r < 16 else -1)
+         for q in range(4)]
+    return np.concatenate(F)
+
+
+def gate_dinput_frag_index(K):
+    """(4*512,) int32: W0^T of the gate (rows = the 6 inputs, k = 64 hidden):
+    dL/dinput = W0^T dL/dH0 (rn_gate_bwd's input gradient)."""
+    sizes, offs = _gate_tables(K)
+    F = [_frag(lambda r, h, j, q=q: _w("w0", _kin(q, h, j), r, sizes, offs)) for q in range(4)]
+    return np.concatenate(F)
+
+
 def _dw_tile(fn):
     out = np.empty(1024, dtype=np.int16)
     for i in range(16):

@@ -130,15 +130,72 @@ class _FieldFn(torch.autograd.Function):
         xyzs, dirs = ctx.saved_tensors
         model, ind = ctx.model, ctx.ind
         dev = xyzs.device
-        grid_grad = torch.zeros_like(model.xyz_encoder.params)
-        dw = torch.zeros_like(model.mlp_params)
-        if xyzs.shape[0] > 0:
-            ds = torch.zeros(xyzs.shape[0], device=dev) if dsigma is None else dsigma.float().contiguous()
-            dr = torch.zeros(xyzs.shape[0], 3, device=dev) if drgb is None else drgb.float().contiguous()
-            model._launch_field(False, xyzs, dirs, ind, dsigma=ds, drgb=dr, grid_grad=grid_grad,
-                                dw=dw, feat=ctx.feat)
+        n = xyzs.shape[0]
+        need_x, need_d, need_g, need_w = ctx.needs_input_grad[:4]
+        grid_grad = torch.zeros_like(model.xyz_encoder.params) if need_g else None
+        dw = torch.zeros_like(model.mlp_params) if need_w else None
+        dx = torch.zeros_like(xyzs) if need_x else None
+        dd = torch.zeros_like(dirs) if need_d else None
+        if n > 0:
+            ds = torch.zeros(n, device=dev) if dsigma is None else dsigma.float().contiguous()
+            dr = torch.zeros(n, 3, device=dev) if drgb is None else drgb.float().contiguous()
+            if need_g or need_w:
+                gg = grid_grad if grid_grad is not None else torch.zeros_like(model.xyz_encoder.params)
+                ww = dw if dw is not None else torch.zeros_like(model.mlp_params)
+                model._launch_field(False, xyzs, dirs, ind, dsigma=ds, drgb=dr, grid_grad=gg,
+                                    dw=ww, feat=ctx.feat)
+            if need_x or need_d:
+                # tcnn's modules back-propagate into their inputs (with
+                # --optimize_ext, train_ml.py:90-93): positions and directions
+                xg = dx if dx is not None else torch.empty_like(xyzs)
+                dg = dd if dd is not None else torch.empty_like(dirs)
+                model._launch_dinput(xyzs, dirs, ind, ds, dr, xg, dg, feat=ctx.feat)
         ctx.feat = None
-        return None, None, grid_grad, dw, None, None
+        return dx, dd, grid_grad, dw, None, None
+
+
+class _DensityFn(torch.autograd.Function):
+    """MNGP.density on rn_field_density.  Backward: the sigma path through the
+    full field backward (rgb seeds zero) and, for x, rn_field_dinput.  The
+    geo features are returned detached (non-differentiable): in the reference
+    only forward() consumes them with a gradient, and forward() here runs the
+    whole field in one kernel."""
+
+    @staticmethod
+    def forward(ctx, x, grid_params, mlp_params, model, ind, return_feat):
+        x = x.float().contiguous()
+        n = x.shape[0]
+        sigma = torch.empty(n, device=x.device)
+        feat = torch.empty(n, 16, device=x.device) if return_feat else None
+        if n > 0:
+            model._launch_density(x, ind, sigma, feat)
+        ctx.save_for_backward(x)
+        ctx.model, ctx.ind = model, ind
+        if feat is None:
+            feat = torch.empty(0, 16, device=x.device)
+        ctx.mark_non_differentiable(feat)
+        return sigma, feat
+
+    @staticmethod
+    def backward(ctx, dsigma, dfeat):
+        (x,) = ctx.saved_tensors
+        model, ind = ctx.model, ctx.ind
+        n = x.shape[0]
+        need_x, need_g, need_w = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2]
+        gg = torch.zeros_like(model.xyz_encoder.params) if need_g else None
+        ww = torch.zeros_like(model.mlp_params) if need_w else None
+        dx = torch.zeros_like(x) if need_x else None
+        if n > 0 and dsigma is not None:
+            ds = dsigma.float().contiguous()
+            d = torch.ones_like(x)                      # no rgb seed: directions unused
+            dr = torch.zeros(n, 3, device=x.device)
+            if need_g or need_w:
+                model._launch_field(False, x, d, ind, dsigma=ds, drgb=dr,
+                                    grid_grad=gg if gg is not None else torch.zeros_like(model.xyz_encoder.params),
+                                    dw=ww if ww is not None else torch.zeros_like(model.mlp_params))
+            if need_x:
+                model._launch_dinput(x, d, ind, ds, dr, dx, torch.empty_like(x))
+        return dx, gg, ww, None, None, None
 
 
 class MNGP(nn.Module):
@@ -198,6 +255,37 @@ class MNGP(nn.Module):
             self._frags_ver = _param_key(p)
         return self._frags
 
+    def packed_dinput_frags(self):
+        """f16 fragments of every sub-NeRF's rgb-net SH columns, transposed
+        (K, 4*512) halfs: the input-gradient kernel's dL/dSH."""
+        p = self.mlp_params
+        if (getattr(self, "_dfrags", None) is None or self._dfrags.device != p.device
+                or self._dfrags_ver != _param_key(p)):
+            idx = _DeviceTables.get("field_dinput_frags", p.device, LY.field_dinput_frag_index)
+            if getattr(self, "_dfrags", None) is None or self._dfrags.device != p.device:
+                self._dfrags = torch.empty(self.size, idx.numel(), dtype=torch.float16,
+                                           device=p.device)
+            lib().pack_f16(p.data_ptr(), LY.FIELD_PARAMS, idx.data_ptr(), idx.numel(), self.size,
+                           idx.numel(), self._dfrags.data_ptr(), _stream(p.device))
+            self._dfrags_ver = _param_key(p)
+        return self._dfrags
+
+    def _launch_dinput(self, xyzs, dirs, ind, dsigma, drgb, dxyz, ddir, feat=None):
+        """dL/dxyzs, dL/ddirs of forward(xyzs, dirs, ind) (rn_field_dinput)."""
+        frags = self.packed_frags()
+        dfr = self.packed_dinput_frags()
+        grid16 = self.xyz_encoder.params_f16()
+        lo, lh, lr, ls = self.xyz_encoder.level_ptrs()
+        n = xyzs.shape[0]
+        nb = max(1, min(2048, (n + 127) // 128))
+        lib().field_dinput(xyzs.data_ptr(), dirs.data_ptr(), n, None, None, None, None, None, None,
+                           1, grid16.data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
+                           self._h_ext.ctypes.data,
+                           frags.data_ptr() + ind * frags.shape[1] * 2,
+                           dfr.data_ptr() + ind * dfr.shape[1] * 2, dsigma.data_ptr(),
+                           drgb.data_ptr(), None if feat is None else feat.data_ptr(),
+                           dxyz.data_ptr(), ddir.data_ptr(), nb, _stream(xyzs.device))
+
     def _launch_field(self, fwd, xyzs, dirs, ind, sigma=None, rgb=None, dsigma=None, drgb=None,
                       grid_grad=None, dw=None, blocks=None, feat=None):
         dev = xyzs.device
@@ -222,12 +310,20 @@ class MNGP(nn.Module):
 
     # ------------------------------------------------------------ reference API
     def density(self, x, ind, return_feat=False):
-        """networks.py:291-309"""
-        if return_feat:
-            raise NotImplementedError("return_feat: use forward(x, d, ind)")
-        d = torch.ones_like(x)
-        sigma, _ = _FieldFn.apply(x, d, self.xyz_encoder.params, self.mlp_params, self, ind)
-        return sigma
+        """networks.py:291-309: hash grid + geo MLP only (rn_field_density);
+        returns sigmas (N), and with return_feat also h[:, 1:17] (N, 16), the
+        geo features the rgb net takes (fp32 of tcnn's f16 values)."""
+        sigma, feat = _DensityFn.apply(x, self.xyz_encoder.params, self.mlp_params, self, ind,
+                                       bool(return_feat))
+        return (sigma, feat) if return_feat else sigma
+
+    def _launch_density(self, x, ind, sigma, feat):
+        frags = self.packed_frags()
+        lo, lh, lr, ls = self.xyz_encoder.level_ptrs()
+        lib().field_density(x.data_ptr(), x.shape[0], self.xyz_encoder.params_f16().data_ptr(),
+                            lo, lh, lr, ls, self._h_min.ctypes.data, self._h_ext.ctypes.data,
+                            frags.data_ptr() + ind * frags.shape[1] * 2, sigma.data_ptr(),
+                            None if feat is None else feat.data_ptr(), _stream(x.device))
 
     def forward(self, x, d, ind, **kwargs):
         """networks.py:311-328 -> sigmas (N), rgbs (N,3)"""
@@ -361,19 +457,24 @@ class _GateFn(torch.autograd.Function):
         g = ctx.gate_mod
         dw = torch.zeros_like(g.params)
         B = x.shape[0]
+        # tcnn's Network back-propagates into its input when it requires grad
+        # (rays_o / rays_d under --optimize_ext)
+        dx = torch.zeros_like(x) if ctx.needs_input_grad[0] else None
         if B > 0 and dgate is not None:
             frags = g.packed_frags()
+            dfr = g.packed_dinput_frags() if dx is not None else None
             nb = max(1, min(128, (B + 127) // 128))
             lib().gate_bwd(x.data_ptr(), x.data_ptr() + 12, 6, B, g.out_dim, frags.data_ptr(),
-                           dgate.float().contiguous().data_ptr(), dw.data_ptr(), dw.numel(), nb,
-                           _stream(x.device))
-        return None, dw, None
+                           dgate.float().contiguous().data_ptr(), dw.data_ptr(), dw.numel(),
+                           None if dfr is None else dfr.data_ptr(),
+                           None if dx is None else dx.data_ptr(), nb, _stream(x.device))
+        return dx, dw, None
 
 
 class Ray_Gate(nn.Module):
     """networks.py:1070-1097: FullyFusedMLP 6 -> 64x4 -> K (ReLU, no bias) +
     softmax(dim=1); importance = gate.sum(0); top_k_indices = None.
-    Note: like the reference, gradients do not flow into the input x."""
+    Gradients flow into the input x when it requires grad, as through tcnn."""
 
     def __init__(self, out_dim, type="ray", seed=None):
         super().__init__()
@@ -400,6 +501,20 @@ class Ray_Gate(nn.Module):
                            self._frags.data_ptr(), _stream(p.device))
             self._frags_ver = _param_key(p)
         return self._frags
+
+    def packed_dinput_frags(self):
+        """f16 A fragments of W0^T (the input gradient of rn_gate_bwd)."""
+        p = self.params
+        if (getattr(self, "_dfrags", None) is None or self._dfrags.device != p.device
+                or self._dfrags_ver != _param_key(p)):
+            idx = _DeviceTables.get(f"gate_dinput_frags_{self.out_dim}", p.device,
+                                    lambda: LY.gate_dinput_frag_index(self.out_dim))
+            if getattr(self, "_dfrags", None) is None or self._dfrags.device != p.device:
+                self._dfrags = torch.empty(idx.numel(), dtype=torch.float16, device=p.device)
+            lib().pack_f16(p.data_ptr(), p.numel(), idx.data_ptr(), idx.numel(), 1, idx.numel(),
+                           self._dfrags.data_ptr(), _stream(p.device))
+            self._dfrags_ver = _param_key(p)
+        return self._dfrags
 
     def forward(self, x, warmup=False):
         gate, _ = _GateFn.apply(x, self.params, self)

@@ -121,3 +121,105 @@ def test_gate_forward_backward(cuda, K):
     e = np.linalg.norm(a - b) / np.linalg.norm(b)
     print(f"gate K={K}: grad rel {e:.2e}")
     assert e <= 1.5e-3        # measured <= 5.2e-4
+
+
+def _seeds(n, seed):
+    rng = np.random.default_rng(seed)
+    return rng.normal(0, 1, n).astype(np.float32), rng.normal(0, 1, (n, 3)).astype(np.float32)
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_field_input_grad(cuda, scale):
+    """dL/dxyz and dL/ddir of MNGP.forward (rn_field_dinput) vs autograd of the
+    fp32 oracle: the hash grid's trilinear-weight derivative (clip mask at the
+    box faces), d/|d| and the SH Jacobian through the f16 MLP chain.  Points
+    include some outside the box (zero gradient) and unnormalised directions."""
+    m = _model(cuda, scale)
+    n = 4000
+    x, d = _inputs(n, scale, seed=5)
+    d = d * np.random.default_rng(6).uniform(0.5, 2.0, (n, 1)).astype(np.float32)
+    ds, dr = _seeds(n, 7)
+    ind = 1
+    xt = torch.from_numpy(x).to(cuda).requires_grad_(True)
+    dt = torch.from_numpy(d).to(cuda).requires_grad_(True)
+    sig, rgb = m(xt, dt, ind)
+    torch.autograd.backward([sig, rgb], [torch.from_numpy(ds).to(cuda), torch.from_numpy(dr).to(cuda)])
+    lv = fo.grid_levels(scale)
+    gp = m.xyz_encoder.params.detach().cpu().view(-1, 2).half().float()
+    from oracle.ml_oracle import _split_field
+    xo = torch.from_numpy(x).requires_grad_(True)
+    do = torch.from_numpy(d).requires_grad_(True)
+    osig, orgb = fo.field_forward(xo, do, gp, _split_field(m.mlp_params.detach().cpu()[ind]), lv,
+                                  m.xyz_min.cpu(), m.xyz_max.cpu())
+    torch.autograd.backward([osig, orgb], [torch.from_numpy(ds), torch.from_numpy(dr)])
+    gx, gd = xt.grad.cpu().numpy(), dt.grad.cpu().numpy()
+    ox, od = xo.grad.numpy(), do.grad.numpy()
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    outside = np.any(np.abs(x) > scale, 1)
+    print(f"field input grad scale {scale}: dxyz rel {rel(gx, ox):.2e}, ddir rel {rel(gd, od):.2e}, "
+          f"{outside.sum()} points outside")
+    assert np.all(gx[outside][np.abs(x[outside]) > scale] == 0)
+    assert rel(gx, ox) <= 1e-3 and rel(gd, od) <= 1e-3          # measured <= 3.5e-4
+    # the parameter gradients are unchanged by also asking for input gradients
+    assert torch.isfinite(m.mlp_params.grad).all() and m.mlp_params.grad.abs().max() > 0
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_density_return_feat(cuda, scale):
+    """MNGP.density(x, ind, return_feat) on rn_field_density (grid + geo MLP
+    only): sigma is bit-identical to the full forward's; sigma and the geo
+    features match the oracle; dL/dx of the density matches autograd."""
+    m = _model(cuda, scale)
+    n = 3000
+    x, d = _inputs(n, scale, seed=11)
+    ind = 0
+    xt = torch.from_numpy(x).to(cuda)
+    with torch.no_grad():
+        sig, feat = m.density(xt, ind, return_feat=True)
+        sig_full, _ = m(xt, torch.from_numpy(d).to(cuda), ind)
+        sig_only = m.density(xt, ind)
+    assert torch.equal(sig, sig_full) and torch.equal(sig, sig_only)
+    assert feat.shape == (n, 16)
+    lv = fo.grid_levels(scale)
+    gp = m.xyz_encoder.params.detach().cpu().view(-1, 2).half().float()
+    from oracle.ml_oracle import _split_field
+    xo = torch.from_numpy(x).requires_grad_(True)
+    osig, ofeat = fo.density_forward(xo, gp, _split_field(m.mlp_params.detach().cpu()[ind]), lv,
+                                     m.xyz_min.cpu(), m.xyz_max.cpu())
+    e_sig = np.abs(sig.cpu().numpy() - osig.detach().numpy()) / (1e-2 + np.abs(osig.detach().numpy()))
+    e_feat = np.abs(feat.cpu().numpy() - ofeat.detach().numpy())
+    print(f"density scale {scale}: sigma rel {e_sig.max():.2e}, feat L_inf {e_feat.max():.2e}")
+    assert e_sig.max() <= 1e-4 and e_feat.max() <= 2e-4         # measured 1.9e-5, 6.1e-5
+    # gradient through the density w.r.t. x and the parameters
+    ds, _ = _seeds(n, 12)
+    xg = xt.clone().requires_grad_(True)
+    m.zero_grad()
+    m.density(xg, ind).backward(torch.from_numpy(ds).to(cuda))
+    osig.backward(torch.from_numpy(ds))
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    e = rel(xg.grad.cpu().numpy(), xo.grad.numpy())
+    print(f"density scale {scale}: dx rel {e:.2e}")
+    assert e <= 1e-3                                               # measured <= 3.0e-4
+    assert m.mlp_params.grad[ind, 3136:].abs().max() == 0      # rgb net untouched
+    assert m.mlp_params.grad[ind, :3136].abs().max() > 0
+
+
+@pytest.mark.parametrize("K", [2, 8])
+def test_gate_input_grad(cuda, K):
+    """dL/dinput of the gate (tcnn Network backward into cat(rays_o, rays_d))."""
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6, scale=0.3)[0]))
+    g = g.to(cuda)
+    o, d = S.rays(2000, 16.0)
+    x = np.concatenate([o, d], 1)
+    xt = torch.from_numpy(x).to(cuda).requires_grad_(True)
+    gate, _, _ = g(xt)
+    dg = np.random.default_rng(3).normal(0, 1, (2000, K)).astype(np.float32)
+    gate.backward(torch.from_numpy(dg).to(cuda))
+    from oracle.ml_oracle import _split_gate
+    xo = torch.from_numpy(x).requires_grad_(True)
+    fo.gate_forward(xo, _split_gate(g.params.detach().cpu(), K)).backward(torch.from_numpy(dg))
+    e = float(np.linalg.norm(xt.grad.cpu().numpy() - xo.grad.numpy()) / np.linalg.norm(xo.grad.numpy()))
+    print(f"gate K={K}: input grad rel {e:.2e}")
+    assert e <= 1.5e-3                                             # measured <= 6.1e-4

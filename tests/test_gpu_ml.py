@@ -19,7 +19,7 @@ from radnerf_amd import synthetic as S
 from radnerf_amd.fused import ml_render_fused, get_renderer
 from radnerf_amd.networks import MNGP, Ray_Gate
 from radnerf_amd.rendering import ml_render
-from parity import LAYERS, check_grads  # noqa: F401
+from parity import LAYERS, check_grads, rel as _rel  # noqa: F401
 
 pytestmark = pytest.mark.gpu
 
@@ -362,3 +362,34 @@ def test_int_grad_matches_fp32(cuda, B, K, scale):
     assert torch.equal(gi[0], gi2[0])
     for a, b in zip(gi[1:], gf[1:]):
         assert ((a - b).norm() / b.norm()) <= 1e-5
+
+
+@pytest.mark.parametrize("scale,K,B", [(0.5, 2, 256), (16.0, 4, 256)])
+def test_input_grads_vs_oracle(cuda, scale, K, B):
+    """--optimize_ext (train_ml.py:90-93): rays_o / rays_d require grad.  The
+    gradients reach them through the gate input, the field's positions and
+    directions (rn_field_dinput) and RayMarcher.backward (rn_ml_march_bw /
+    rn_raymarching_train_bw): fused chain and drop-in chain vs the oracle's
+    autograd + segment sums (custom_functions.py:102-112)."""
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    out = {}
+    for name, fn in (("fused", ml_render_fused), ("dropin", ml_render)):
+        m.zero_grad(); g.zero_grad()
+        ot, dt = to(o).requires_grad_(True), to(d).requires_grad_(True)
+        res = fn(m, g, ot, dt, dt, noise=to(noise), exp_step_factor=esf)
+        torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]], [to(s) for s in seeds])
+        out[name] = (ot.grad.cpu().numpy(), dt.grad.cpu().numpy(), m.mlp_params.grad.clone())
+    ores = ml_oracle.ml_train_step(o, d, bits, noise, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                   m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale,
+                                   seeds=seeds, input_grads=True)
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+    for name, (go, gd, mg) in out.items():
+        eo, ed = rel(go, ores["drays_o"]), rel(gd, ores["drays_d"])
+        print(f"input grads {name} scale {scale} K {K}: drays_o rel {eo:.2e}, drays_d rel {ed:.2e}")
+        assert eo <= 3e-3 and ed <= 3e-3          # measured <= 1.0e-3
+        # asking for input gradients leaves the parameter gradients as they were
+        assert _rel(mg.cpu().numpy(), ores["mlp_grad"]) <= 4e-3
+    assert rel(out["fused"][0], out["dropin"][0]) <= 1e-3
+    assert rel(out["fused"][1], out["dropin"][1]) <= 1e-3

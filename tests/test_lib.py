@@ -57,7 +57,7 @@ def test_arg_validation_without_gpu():
     with pytest.raises(RuntimeError, match="null pointer"):
         L.packbits(None, 8, 0.5, None, None)
     with pytest.raises(RuntimeError, match="n_params mismatch"):
-        L.gate_bwd(None, None, 3, 10, 2, None, None, None, 5, 1, None)
+        L.gate_bwd(None, None, 3, 10, 2, None, None, None, 5, None, None, 1, None)
 
 
 def test_vren_checks_like_reference():
