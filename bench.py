@@ -48,6 +48,11 @@ MFMA_F16_PEAK_TFLOPS = 2500.0        # MI355X dense f16/bf16 (MI355X_MICROARCH.m
 ATOMIC_PEAK_GREQ = 1.3e12 / 64 / 1e9
 
 
+def workload_key(K, scale, rays, occupancy):
+    """Key of a workload's PMC pass in profiles/traffic.json (tools/pmc_traffic.py)."""
+    return f"K{K}_s{float(scale):g}_B{rays}_p{float(occupancy):.2f}"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -60,11 +65,17 @@ def parse():
     ap.add_argument("--cpu-rays", type=int, default=512,
                     help="rays in the bounded CPU-oracle sample: CPU baseline timing and the "
                          "rgb L_inf check (0 = skip)")
+    ap.add_argument("--cpu-sample-rays", type=int, default=256,
+                    help="rays of the workload in the timed CPU-baseline sample")
+    ap.add_argument("--cpu-reps", type=int, default=10,
+                    help="timed CPU-baseline steps (median; after 3 warm-up steps)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic.json"))
     ap.add_argument("--train-step", type=int, default=1,
                     help="also time the full train step (loss + Adam); 0 = skip")
     ap.add_argument("--dropin-step", type=int, default=1,
                     help="also time the step through the drop-in rendering.ml_render chain; 0 = skip")
+    ap.add_argument("--density-update", type=int, default=1,
+                    help="also time the occupancy-grid update (warm-up and sampled); 0 = skip")
     ap.add_argument("--split-bwd", action="store_true",
                     help="backward with one model per block (rn_field_bwd) instead of the "
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
@@ -163,6 +174,15 @@ def main():
     r.trace = False
     kt = r.kernel_times_ms()
     kt["field_bwd"] = bwd_live
+    # gate_bwd runs on a side stream beside field_bwd (hidden there, but its
+    # events then span the wait for CUs): its own duration, in line
+    at = r.gate_bwd_at
+    r.gate_bwd_at, r.trace, r.events = "main", {"gate_bwd"}, {}
+    for i in range(3):
+        step(i)
+    samples_acc.copy_(saved)
+    r.gate_bwd_at, r.trace = at, False
+    kt["gate_bwd"] = r.kernel_times_ms()["gate_bwd"]
 
     # forward-only rate (north_star's forward target), timed after the headline
     # region with the same barrier/sync bracketing; not part of `value`
@@ -251,6 +271,25 @@ def main():
         dropin = {"value": round(int(samples_acc) / d_el / 1e6, 2), "unit": "Msamples/s",
                   "ms_per_step": round(d_el / args.steps * 1e3, 4),
                   "path": "rendering.ml_render (drop-in autograd chain), fwd+bwd"}
+    # occupancy-grid maintenance (train_ml.py:174-177;
+    # every 16 steps, outside the metric): the warm-up update over all
+    # 128^3 x cascades cells of every sub-NeRF, and the regular update over
+    # 128^3/4 uniform + 128^3/4 occupied cells, rank-consistent stream
+    density = None
+    if args.density_update:
+        thr = 0.01 * 1024 / 3 ** 0.5
+        dms = {}
+        for name, warm in (("warmup_all_cells", True), ("sampled_cells", False)):
+            rdist.update_density_grid(model, thr, 0, warmup=warm)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(3):
+                rdist.update_density_grid(model, thr, i + 1, warmup=warm)
+            torch.cuda.synchronize()
+            dms[name] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+        cells = model.cascades * 128 ** 3
+        density = {"ms": dms, "cells_per_model_warmup": cells, "models": K,
+                   "kernel": "rn_field_density (hash grid + geo MLP) + morton / packbits"}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:
@@ -265,19 +304,26 @@ def main():
     samples_per_step_rank = int(samples_acc) / args.steps
     bwd_ms = kms.get("field_bwd", float("nan"))
     achieved = samples_per_step_rank * FIELD_BWD_BYTES_PER_SAMPLE / (bwd_ms * 1e-3) / 1e9
-    traffic, atom_req, pmc_samples = None, None, None
-    if os.path.exists(args.traffic_json):
+    # PMC figures only for a workload that has its own pass (tools/pmc_traffic.py
+    # --merge keys them by K, scale, rays and occupancy); per launch, scaled by
+    # this run's sample count where it differs from the profiled run's
+    traffic, atom_req, pmc_samples, pmc_key = None, None, None, workload_key(K, scale, B,
+                                                                             args.occupancy)
+    if os.path.exists(args.traffic_json) and not args.split_bwd:
         try:
             with open(args.traffic_json) as f:
-                tj = json.load(f)
-            traffic = tj.get("field_bwd_bytes_per_launch")
-            atom_req = tj.get("field_bwd_atomic_requests")
-            pmc_samples = tj.get("samples_per_launch") or samples_per_step_rank
-        except (OSError, ValueError):
+                tj = json.load(f).get("workloads", {}).get(pmc_key)
+            if tj:
+                pmc_samples = tj.get("samples_per_launch") or samples_per_step_rank
+                traffic = tj.get("field_bwd_bytes_per_launch")
+                if traffic:
+                    traffic = round(traffic * samples_per_step_rank / pmc_samples)
+                atom_req = tj.get("field_bwd_atomic_requests")
+        except (OSError, ValueError, AttributeError):
             traffic = None
     roofline = {"kernel": "field_bwd", "bound": "hbm", "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
+                "traffic": traffic, "traffic_source": pmc_key if traffic else None,
                 "algorithmic_bytes_per_sample": FIELD_BWD_BYTES_PER_SAMPLE,
                 "samples_per_launch": round(samples_per_step_rank),
                 "avg_launch_ms": round(bwd_ms, 4),
@@ -316,6 +362,7 @@ def main():
                "data": "synthetic",
                "config": {"workload": workload,
                           "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,
+                          "occupancy": args.occupancy,
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": f"pinned{world}" if args.pinned else f"dp{world}"},
@@ -324,6 +371,7 @@ def main():
                "forward_only": fwd_only,
                "train_step": train,
                "dropin_step": dropin,
+               "density_update": density,
                # MFMA use: algorithmic MLP flops (56,832 per sample
                # fwd+bwd, unpadded) at `value`, against the dense f16 peak
                "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),
@@ -335,11 +383,39 @@ def main():
         dist.destroy_process_group()
 
 
+def _cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _time_oracle(args_fn, reps, warm):
+    """median wall time of `reps` oracle steps after `warm` untimed ones"""
+    from oracle import ml_oracle
+    ts, res = [], None
+    for i in range(warm + reps):
+        t0 = time.perf_counter()
+        res = ml_oracle.ml_train_step(*args_fn())
+        if i >= warm:
+            ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), res
+
+
 def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, bg, esf, scale,
                 seeds_np):
     """rgb L_inf of the GPU path vs the CPU oracle on the first rays of the
-    workload, and the CPU-oracle throughput on a bounded sample."""
+    workload, and the CPU baseline: the oracle (C march /
+    composite with OpenMP over rays + torch-CPU fp32 field) timed as 3 untimed
+    + 10 timed fwd+bwd steps, median, on (a) a bounded sample of this
+    workload and (b) config C1 (single NGP, 1024 rays, scale 0.5)."""
     from oracle import ml_oracle
+    from radnerf_amd import layout as LY
+    from radnerf_amd import synthetic as S
     n = args.cpu_rays
     rgb, _, _, _, _ = r.forward(rays_o, rays_d, rays_d, noise, bg, 1e-4, esf)
     rgb = rgb.cpu().numpy()
@@ -347,22 +423,40 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
     mp = model.mlp_params.detach().cpu().numpy()
     ap = gate.params.detach().cpu().numpy()
     nz = noise.cpu().numpy()
-    threads = min(16, os.cpu_count() or 1)
+    threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
-    # one bounded oracle step (fwd + bwd) serves both legs: its forward rgb is
-    # compared with the GPU's rgb for the same rays, its wall time is the baseline
-    c = n
-    sd = tuple(np.ascontiguousarray(s[:c]) for s in seeds_np)
-    t0 = time.perf_counter()
-    res = ml_oracle.ml_train_step(o_np[:c], d_np[:c], bits, np.ascontiguousarray(nz[:, :c]),
-                                  gp, mp, ap, scale, seeds=sd)
-    dt = time.perf_counter() - t0
-    rgb_linf = float(np.abs(res["rgb"] - rgb[:c]).max())
-    cpu = {"value": round(res["total"] / dt / 1e6, 5), "unit": "Msamples/s",
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    # correctness leg: the GPU's rgb on the first n rays against the oracle's
+    res = ml_oracle.ml_train_step(o_np[:n], d_np[:n], bits, np.ascontiguousarray(nz[:, :n]),
+                                  gp, mp, ap, scale, seeds=tuple(np.ascontiguousarray(x[:n])
+                                                                 for x in seeds_np))
+    rgb_linf = float(np.abs(res["rgb"] - rgb[:n]).max())
+    # (a) bounded sample of this workload
+    c = args.cpu_sample_rays
+    sd = tuple(np.ascontiguousarray(x[:c]) for x in seeds_np)
+    nzc = np.ascontiguousarray(nz[:, :c])
+    t_a, res_a = _time_oracle(lambda: (o_np[:c], d_np[:c], bits, nzc, gp, mp, ap, scale, sd),
+                              args.cpu_reps, 3)
+    # (b) C1: single NGP (K = 1), 1024 rays, scale 0.5, the same synthetic recipe
+    lv = LY.grid_levels(0.5)
+    g1 = S.grid_params(lv["n_entries"], seed=3).reshape(-1, 2)
+    m1 = S.mlp_params(1, LY.FIELD_PARAMS, seed=3)
+    b1 = S.bitfields(1, 1, p=args.occupancy, seed=1)
+    o1, d1 = S.rays(1024, 0.5, seed=11)
+    n1 = S.noise(1, 1024, seed=12)
+    s1 = S.loss_seeds(1024, 1, seed=13)
+    gate1 = np.zeros(LY.gate_params(1), np.float32)        # softmax over one model = 1
+    t_b, res_b = _time_oracle(lambda: (o1, d1, b1, n1, g1, m1, gate1, 0.5, s1), args.cpu_reps, 3)
+    cpu = {"value": round(res_a["total"] / t_a / 1e6, 5), "unit": "Msamples/s",
            "cores": threads, "kind": "port",
-           "sample": f"{c} rays x K={args.models} ({res['total']} samples) of the same workload, "
-                     f"one fwd+bwd step of oracle/ml_oracle.py (C march/composite + torch-CPU "
-                     f"fp32 field, {threads} threads), {dt:.1f} s"}
+           "sample": f"{c} rays x K={args.models} ({res_a['total']} samples) of the same workload, "
+                     f"fwd+bwd step of oracle/ml_oracle.py (C march/composite, OpenMP over rays; "
+                     f"torch-CPU fp32 field), median of {args.cpu_reps} after 3 warm-up, "
+                     f"{t_a:.2f} s/step",
+           "c1": {"value": round(res_b["total"] / t_b / 1e6, 5), "unit": "Msamples/s",
+                  "sample": f"C1: single NGP, 1024 rays, scale 0.5 ({res_b['total']} samples), "
+                            f"median of {args.cpu_reps} after 3 warm-up, {t_b:.2f} s/step"},
+           "nproc": os.cpu_count(), "cpu_model": _cpu_model_name()}
     return rgb_linf, cpu
 
 

@@ -5,8 +5,13 @@ RCCL all-reduce over xGMI per step (torch.distributed backend "nccl" = RCCL
 on ROCm; "gloo" for the CPU tests).
 
 The reference is single-GPU (train_ml.py:295-304); this is the build's
-addition.  Bitfields must stay identical across ranks: `broadcast_buffers`
-ships rank 0's copy (C x 256 KiB per sub-NeRF) after a density-grid update.
+addition.  Bitfields must stay identical across ranks.  `update_density_grid`
+keeps them so without a collective: every rank draws the update's cells and
+jitter from a generator seeded by (seed, step), and the parameters are
+identical after each step's all-reduce + Adam, so the deterministic density
+kernel produces the same grids.  `broadcast_buffers` (rank 0's copy, C x 256
+KiB per sub-NeRF) remains for callers that update with torch's default
+stream.
 """
 import os
 
@@ -83,3 +88,18 @@ def broadcast_buffers(module, src=0):
         for name, b in module.named_buffers():
             if "density" in name:
                 dist.broadcast(b, src)
+
+
+def step_generator(device, seed, step):
+    """A generator on `device` seeded identically on every rank for `step`."""
+    g = torch.Generator(device=device)
+    g.manual_seed((int(seed) * 1000003 + int(step)) & 0x7FFFFFFFFFFFFFFF)
+    return g
+
+
+def update_density_grid(model, density_threshold, step, warmup=False, seed=0, decay=0.95):
+    """train_ml.py:174-177 (model.update_density_grid every update_interval
+    steps) made rank-consistent: the cell draws and jitter come from
+    step_generator(seed, step), identical on every rank."""
+    g = step_generator(model.mlp_params.device, seed, step)
+    model.update_density_grid(density_threshold, warmup=warmup, decay=decay, generator=g)

@@ -160,7 +160,11 @@ class FusedMLRenderer:
         # and where: "field" side stream beside field_bwd, "early" side stream
         # beside composite_bw, "main" in line before field_bwd
         self.gate_grad_here = True
-        self.gate_bwd_at = "field"
+        # "early": beside composite_bw, before field_bwd's persistent blocks
+        # occupy every CU (beside field_bwd it waited for them: its events
+        # spanned 1.3-3.7 ms for a 0.09 ms kernel).  C3 step: early 5.037,
+        # field 5.045, main 5.117 ms (tools/step_variants.py, r02)
+        self.gate_bwd_at = "early"
         # input gradients (dL/drays_o, dL/drays_d) in backward(): set by
         # _MLRenderFn when the rays require grad (--optimize_ext)
         self.input_grad = False

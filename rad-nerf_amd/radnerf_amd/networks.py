@@ -336,17 +336,19 @@ class MNGP(nn.Module):
         return [(indices, self.grid_coords)] * self.cascades
 
     @torch.no_grad()
-    def sample_uniform_and_occupied_cells(self, M, density_threshold, ind):
-        """networks.py:345-372"""
+    def sample_uniform_and_occupied_cells(self, M, density_threshold, ind, generator=None):
+        """networks.py:345-372 (generator: the random stream; None = torch's
+        default, as the reference)"""
         cells = []
         density_grid = getattr(self, f"density_grid_{ind}")
         for c in range(self.cascades):
             coords1 = torch.randint(self.grid_size, (M, 3), dtype=torch.int32,
-                                    device=density_grid.device)
+                                    device=density_grid.device, generator=generator)
             indices1 = vren.morton3D(coords1).long()
             indices2 = torch.nonzero(density_grid[c] > density_threshold)[:, 0]
             if len(indices2) > 0:
-                rand_idx = torch.randint(len(indices2), (M,), device=density_grid.device)
+                rand_idx = torch.randint(len(indices2), (M,), device=density_grid.device,
+                                         generator=generator)
                 indices2 = indices2[rand_idx]
                 coords2 = vren.morton3D_invert(indices2.int())
                 cells += [(torch.cat([indices1, indices2]), torch.cat([coords1, coords2]))]
@@ -355,8 +357,16 @@ class MNGP(nn.Module):
         return cells
 
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
-        """networks.py:375-409"""
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False,
+                            generator=None):
+        """networks.py:375-409.  `generator` (a torch.Generator on the model's
+        device) replaces torch's default random stream for the cell draws and
+        the jitter: with ray-batch data parallelism every rank passes one
+        seeded identically (radnerf_amd.dist.update_density_grid), so the
+        ranks draw the same cells and, with identical parameters and
+        deterministic kernels, keep bit-identical grids and bitfields with no
+        collective.  sigma comes from the density-only kernel (rn_field_density:
+        hash grid + geo MLP, networks.py:393-394)."""
         for i in range(self.size):
             density_grid = getattr(self, f"density_grid_{i}")
             density_bitfield = getattr(self, f"density_bitfield_{i}")
@@ -365,14 +375,19 @@ class MNGP(nn.Module):
                 cells = self.get_all_cells()
             else:
                 cells = self.sample_uniform_and_occupied_cells(self.grid_size ** 3 // 4,
-                                                               density_threshold, i)
+                                                               density_threshold, i, generator)
             for c in range(self.cascades):
                 indices, coords = cells[c]
                 s = min(2 ** (c - 1), self.scale)
                 half_grid_size = s / self.grid_size
                 xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
-                xyzs_w += (torch.rand_like(xyzs_w) * 2 - 1) * half_grid_size
-                tmp[c, indices] = self.density(xyzs_w, i)
+                jitter = torch.rand(xyzs_w.shape, device=xyzs_w.device, generator=generator)
+                xyzs_w += (jitter * 2 - 1) * half_grid_size
+                # duplicate cells (the uniform and the occupied draws overlap):
+                # the reference's index_put keeps an arbitrary one of them
+                # (nondeterministic on the GPU); the max is deterministic, so
+                # ranks with identical inputs keep identical grids
+                tmp[c].scatter_reduce_(0, indices, self.density(xyzs_w, i), reduce="amax")
             density_grid = torch.where(density_grid < 0, density_grid,
                                        torch.maximum(density_grid * decay, tmp))
             mean_density = density_grid[density_grid > 0].mean().item()
@@ -428,8 +443,9 @@ class NGP(MNGP):
         return super().forward(x, d, 0)
 
     @torch.no_grad()
-    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False):
-        super().update_density_grid(density_threshold, warmup, decay, erode)
+    def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False,
+                            generator=None):
+        super().update_density_grid(density_threshold, warmup, decay, erode, generator)
 
 
 class _GateFn(torch.autograd.Function):

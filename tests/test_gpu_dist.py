@@ -2,7 +2,8 @@
 bench.py --gpus N runs over RCCL) rehearsed with 2 ranks on one GPU over gloo:
 the averaged flat gradient equals the average of the per-rank gradients
 computed in one process (within 1e-4 of the largest entry: float-atomic
-accumulation order differs)."""
+accumulation order differs); and multi-step training (radnerf_amd.trainer)
+keeps every rank's parameters, density grids and bitfields bit-identical."""
 import json
 import os
 import socket
@@ -24,27 +25,47 @@ def _port():
     return p
 
 
-def test_data_parallel_two_ranks_one_gpu(tmp_path):
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    out = tmp_path / "dp.json"
+def _run_ranks(worker, out, timeout=100):
     port = _port()
     procs = []
     for rank in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                    LOCAL_RANK=str(rank), WORLD_SIZE="2")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "dp_worker.py"),
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", worker),
                                        str(out)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
         try:
-            logs.append(p.communicate(timeout=100)[0].decode(errors="replace"))
+            logs.append(p.communicate(timeout=timeout)[0].decode(errors="replace"))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
             raise
     assert all(p.returncode == 0 for p in procs), logs
-    res = json.loads(out.read_text())
+    return json.loads(out.read_text())
+
+
+def test_data_parallel_two_ranks_one_gpu(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks("dp_worker.py", tmp_path / "dp.json")
     assert res["world"] == 2, res
     assert res["grid_rel"] <= 1e-4 and res["mlp_rel"] <= 1e-4 and res["gate_rel"] <= 1e-4, res
+
+
+def test_data_parallel_training_stays_identical(tmp_path):
+    """radnerf_amd.trainer.Trainer on 2 ranks (one GPU, gloo): 14 steps with
+    density-grid updates every 4 steps (warm-up over every cell, then sampled
+    cells), the fused loss, the flat all-reduce and Adam.  Each rank trains on
+    its own rays; parameters, density grids and bitfields stay bit-identical
+    across the ranks (rank-consistent update stream, no broadcast), and the
+    updates do change the bitfields."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks("train_worker.py", tmp_path / "train.json", timeout=110)
+    print(res)
+    assert res["world"] == 2
+    assert all(res["identical"].values()), res["identical"]
+    assert all(res["bitfields_changed"]), res
+    assert res["finite"]

@@ -1,6 +1,11 @@
 """Reduce rocprofv3 PMC passes to per-launch HBM traffic of the field kernels.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> [<atomic_dir>] > traffic.json
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> [<atomic_dir>] [--merge profiles/traffic.json]
+
+The passes are keyed by workload (K, scale, rays, occupancy; from the bench
+JSON line in <dir>.log): with --merge the entry is written into the
+traffic file under that key, which bench.py looks up for its own workload
+(no figures are reported for a workload without a PMC pass).
 
 Each dir holds run_counter_collection.csv of one `rocprofv3 --pmc <counter>`
 pass over `bench.py` (separate passes: FETCH_SIZE and WRITE_SIZE cannot share
@@ -45,22 +50,36 @@ def per_dispatch(d):
     return out
 
 
+def workload_key(cfg):
+    """bench.py's key of a workload (keep in sync with bench.py workload_key)."""
+    return (f"K{cfg['model_zoo_size']}_s{float(cfg['scale']):g}_B{cfg['rays_per_gpu']}"
+            f"_p{float(cfg.get('occupancy', 0.5)):.2f}")
+
+
 def main():
-    fetch = per_dispatch(sys.argv[1])
-    write = per_dispatch(sys.argv[2])
-    atom = per_dispatch(sys.argv[3]) if len(sys.argv) > 3 and os.path.isdir(sys.argv[3]) else {}
-    samples = None
-    for d in sys.argv[1:3]:
+    argv = list(sys.argv[1:])
+    merge = None
+    if "--merge" in argv:
+        i = argv.index("--merge")
+        merge = argv[i + 1]
+        del argv[i:i + 2]
+    fetch = per_dispatch(argv[0])
+    write = per_dispatch(argv[1])
+    atom = per_dispatch(argv[2]) if len(argv) > 2 and os.path.isdir(argv[2]) else {}
+    samples, cfg = None, None
+    for d in argv[:2]:
         try:
             with open(d.rstrip("/") + ".log") as f:
                 for line in f:
                     if line.startswith('{"metric"'):
-                        samples = json.loads(line)["config"]["samples_per_step_per_gpu"]
+                        cfg = json.loads(line)["config"]
+                        samples = cfg["samples_per_step_per_gpu"]
         except (OSError, ValueError, KeyError):
             pass
-    out = {"samples_per_launch": samples,
+    key = workload_key(cfg) if cfg else "unknown"
+    out = {"workload": key, "samples_per_launch": samples,
            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE / TCC_EA0_ATOMIC, separate passes, "
-                     "bench.py C3 workload; per launch (one launch per step)"}
+                     "bench.py on this workload; per launch (one launch per step)"}
     for k in KERNELS:
         if k not in fetch or k not in write:
             continue
@@ -72,6 +91,16 @@ def main():
             out[f"{k}_atomic_requests"] = round(atom[k])
     json.dump(out, sys.stdout, indent=1)
     print()
+    if merge:
+        try:
+            with open(merge) as f:
+                allw = json.load(f)
+        except (OSError, ValueError):
+            allw = {}
+        allw.setdefault("workloads", {})[key] = out
+        with open(merge, "w") as f:
+            json.dump(allw, f, indent=1)
+            f.write("\n")
 
 
 if __name__ == "__main__":
