@@ -79,8 +79,9 @@ def parse():
     ap.add_argument("--split-bwd", action="store_true",
                     help="backward with one model per block (rn_field_bwd) instead of the "
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
-    ap.add_argument("--max-chunk", type=int, default=1024,
-                    help="merged backward: largest chunk of merged samples per queue grab")
+    ap.add_argument("--max-chunk", type=int, default=None,
+                    help="merged backward: largest chunk of merged samples per queue grab "
+                         "(default: the renderer's, by rays x sub-NeRFs)")
     ap.add_argument("--head-chunk", type=int, default=0,
                     help="merged passes: first chunk per block (0 = none)")
     ap.add_argument("--pinned", action="store_true",
@@ -130,7 +131,8 @@ def main():
     else:
         r = FusedMLRenderer(model, gate, B)
     r.merged_bwd = r.merged_bwd and not args.split_bwd
-    r.max_chunk = args.max_chunk
+    if args.max_chunk:
+        r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
@@ -182,7 +184,9 @@ def main():
         step(i)
     samples_acc.copy_(saved)
     r.gate_bwd_at, r.trace = at, False
-    kt["gate_bwd"] = r.kernel_times_ms()["gate_bwd"]
+    gt_ms = r.kernel_times_ms().get("gate_bwd")
+    if gt_ms:                       # (one sub-NeRF: no gate MLP at all)
+        kt["gate_bwd"] = gt_ms
 
     # forward-only rate (north_star's forward target), timed after the headline
     # region with the same barrier/sync bracketing; not part of `value`
@@ -279,6 +283,9 @@ def main():
     if args.density_update:
         thr = 0.01 * 1024 / 3 ** 0.5
         dms = {}
+        # the update rewrites the occupancy buffers: restore them afterwards
+        # (the oracle leg below marches the workload's original bitfields)
+        saved_buf = {n: b.clone() for n, b in model.named_buffers() if "density" in n}
         for name, warm in (("warmup_all_cells", True), ("sampled_cells", False)):
             rdist.update_density_grid(model, thr, 0, warmup=warm)
             torch.cuda.synchronize()
@@ -287,6 +294,10 @@ def main():
                 rdist.update_density_grid(model, thr, i + 1, warmup=warm)
             torch.cuda.synchronize()
             dms[name] = round((time.perf_counter() - t0) / 3 * 1e3, 3)
+        with torch.no_grad():
+            for n_, b_ in model.named_buffers():
+                if n_ in saved_buf:
+                    b_.copy_(saved_buf[n_])
         cells = model.cascades * 128 ** 3
         density = {"ms": dms, "cells_per_model_warmup": cells, "models": K,
                    "kernel": "rn_field_density (hash grid + geo MLP) + morton / packbits"}

@@ -346,6 +346,12 @@ int rn_morton3d(const int32_t* coords, int64_t n, int32_t* indices, void* stream
 int rn_morton3d_invert(const int32_t* indices, int64_t n, int32_t* coords, void* stream);
 int rn_packbits(const float* density_grid, int64_t n_bytes, float density_threshold,
                 uint8_t* density_bitfield, void* stream);
+/* out[indices[i]] = max(out[indices[i]], values[i]) for non-negative values:
+ * the density update's `tmp[c, indices] = density(...)` (networks.py:393-394)
+ * with duplicate cells resolved deterministically (the reference's
+ * index_put keeps an arbitrary one of them).                                */
+int rn_scatter_max(const int64_t* indices, const float* values, int64_t n, float* out,
+                   void* stream);
 
 #ifdef __cplusplus
 }

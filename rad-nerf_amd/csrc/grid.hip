@@ -48,6 +48,17 @@ k_packbits(int64_t n_bytes, const float* __restrict__ grid, float thr, uint8_t* 
     bits[b] = v;
 }
 
+// tmp[c, indices] = sigma (networks.py:393-394) with duplicate cells resolved
+// by their max, deterministically: sigma >= 0, so the int order of the bits is
+// the float order and one integer atomicMax per value suffices
+__global__ void __launch_bounds__(256)
+k_scatter_max(int64_t n, const int64_t* __restrict__ idx, const float* __restrict__ v,
+              float* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    atomicMax(reinterpret_cast<int*>(out) + idx[i], __float_as_int(fmaxf(v[i], 0.0f)));
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -85,6 +96,16 @@ int rn_packbits(const float* density_grid, int64_t n_bytes, float density_thresh
     k_packbits<<<nblk(n_bytes, 256), 256, 0, (hipStream_t)stream>>>(n_bytes, density_grid,
                                                                      density_threshold,
                                                                      density_bitfield);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_scatter_max(const int64_t* indices, const float* values, int64_t n, float* out,
+                   void* stream) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    if (n == 0) return 0;
+    RN_CHECK_ARG(indices && values && out, "null pointer");
+    k_scatter_max<<<nblk(n, 256), 256, 0, (hipStream_t)stream>>>(n, indices, values, out);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rn_morton3d": [P, I64, P, P],
     "rn_morton3d_invert": [P, I64, P, P],
     "rn_packbits": [P, I64, F32, P, P],
+    "rn_scatter_max": [P, P, I64, P, P],
 }
 
 _lib = None

@@ -145,7 +145,11 @@ class FusedMLRenderer:
         # chunk of merged samples per queue ticket: 1024 keeps a block's staged
         # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
         # 8192 4.50 ms)
-        self.max_chunk = 1024
+        # Small steps want more, smaller chunks (at least a few per block): C1
+        # (K = 1, 1024 rays) 1024 -> 256 is 0.707 -> 0.618 ms per step, C2
+        # (K = 1, 8192 rays) 512 = 1024 (tools/step_variants.py, r02)
+        rk = n_rays * model.size
+        self.max_chunk = 256 if rk <= 1024 else (512 if rk <= 4096 else 1024)
         # exact integer accumulation of the grid gradient (rn_seed_scale +
         # returning u32 atomics with carries + rn_igrad_to_f32): bitwise
         # reproducible grid gradients, but each issue waits for the previous
@@ -214,11 +218,18 @@ class FusedMLRenderer:
         imp = torch.zeros(G, device=rays_o.device)
         side = self._side(rays_o.device)
         main = torch.cuda.current_stream(rays_o.device)
-        frags = g.packed_frags()          # (re)packed on the main stream
-        side.wait_stream(main)
-        self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
-                 frags.data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
-                 max(1, min(256, (B + 127) // 128)), side.cuda_stream, stream=side)
+        if G == 1:
+            # softmax over one sub-NeRF is exactly 1 (and its gradient exactly
+            # 0): single-NGP configs C1 / C2 skip the gate MLP
+            out_gate.fill_(1.0)
+            imp.fill_(float(B))
+            side.wait_stream(main)
+        else:
+            frags = g.packed_frags()          # (re)packed on the main stream
+            side.wait_stream(main)
+            self._ev("gate_fwd", L.gate_fwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
+                     frags.data_ptr(), out_gate.data_ptr(), imp.data_ptr(),
+                     max(1, min(256, (B + 127) // 128)), side.cuda_stream, stream=side)
         bits = self.bitfields()
         march = (rays_o.data_ptr(), rays_d.data_ptr(), m.center.data_ptr(),
                  m.half_size.data_ptr(), NEAR_DISTANCE, noise.data_ptr(), bits.data_ptr(),
@@ -364,9 +375,13 @@ class FusedMLRenderer:
         main = torch.cuda.current_stream(dev)
 
         gate_dx = self._gate_dinput(B, dev) if self.input_grad else None
-        gate_dfr = g.packed_dinput_frags() if gate_dx is not None else None
+        gate_dfr = g.packed_dinput_frags() if gate_dx is not None and G > 1 else None
 
         def gate_bwd(stream):
+            if G == 1:              # d softmax over one model = 0: nothing to add
+                if gate_dx is not None:
+                    gate_dx.zero_()
+                return
             frags = g.packed_frags()
             if stream is side:
                 side.wait_stream(main)

@@ -387,7 +387,9 @@ class MNGP(nn.Module):
                 # the reference's index_put keeps an arbitrary one of them
                 # (nondeterministic on the GPU); the max is deterministic, so
                 # ranks with identical inputs keep identical grids
-                tmp[c].scatter_reduce_(0, indices, self.density(xyzs_w, i), reduce="amax")
+                sig = self.density(xyzs_w, i)
+                lib().scatter_max(indices.contiguous().data_ptr(), sig.data_ptr(), sig.numel(),
+                                  tmp[c].data_ptr(), _stream(sig.device))
             density_grid = torch.where(density_grid < 0, density_grid,
                                        torch.maximum(density_grid * decay, tmp))
             mean_density = density_grid[density_grid > 0].mean().item()

@@ -252,3 +252,23 @@ def test_composite_termination_at_threshold(cuda):
                                              oop, ode, orgb, 1e-4)
     assert np.array_equal(drgb.cpu().numpy() == 0, odrgb == 0)
     assert np.abs(drgb.cpu().numpy() - odrgb).max() <= 1e-4
+
+
+def test_scatter_max_duplicates(cuda):
+    """rn_scatter_max: the density update's tmp[c, indices] = sigma with
+    duplicate cells resolved by their max (numpy reference), deterministic."""
+    from radnerf_amd._lib import lib
+    rng = np.random.default_rng(4)
+    n, m = 300000, 50000
+    idx = rng.integers(0, m, n).astype(np.int64)
+    val = rng.gamma(1.0, 2.0, n).astype(np.float32)
+    ref = np.zeros(m, np.float32)
+    np.maximum.at(ref, idx, val)
+    outs = []
+    for _ in range(2):
+        out = torch.zeros(m, device=cuda)
+        gi, gv = _t(idx, cuda), _t(val, cuda)
+        lib().scatter_max(gi.data_ptr(), gv.data_ptr(), n, out.data_ptr(),
+                          torch.cuda.current_stream(cuda).cuda_stream)
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0], ref) and np.array_equal(outs[1], ref)

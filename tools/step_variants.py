@@ -2,7 +2,7 @@
 fwd+bwd steps with no per-launch events, variants interleaved round by round
 (rule 24 of cdna_hip_programming.md §5.4); prints median ms per step.
 
-usage: [STEP_K=K] python tools/step_variants.py [attr=value[,attr=value]] ...
+usage: [STEP_K=K] [STEP_B=B] python tools/step_variants.py [attr=value[,attr=value]] ...
   e.g. gate_bwd_at=field gate_bwd_at=early gate_bwd_at=main
 """
 import json
@@ -31,7 +31,7 @@ def parse(tok):
 def main():
     variants = sys.argv[1:] or ["gate_bwd_at=field", "gate_bwd_at=early", "gate_bwd_at=main"]
     dev = torch.device("cuda")
-    B, K, steps = 8192, int(os.environ.get("STEP_K", 2)), 10
+    B, K, steps = int(os.environ.get("STEP_B", 8192)), int(os.environ.get("STEP_K", 2)), 10
     m = MNGP(0.5, size=K, seed=3).to(dev)
     g = Ray_Gate(K, seed=4).to(dev)
     bits = S.bitfields(K, 1, p=0.5, seed=1)
