@@ -41,7 +41,15 @@ def _worker(rank, world, port, q):
         m.register_buffer("other", torch.full((2,), rank))
         rdist.broadcast_buffers(m)
         ok_bcast = bool((m.density_bitfield_0 == 0).all()) and int(m.other[0]) == rank
-        q.put((rank, lo, hi, ok_mean, ok_bcast))
+        # the density update's stream: identical draws on every rank for a step,
+        # different draws for different steps
+        g5 = rdist.step_generator("cpu", 7, 5)
+        draw = torch.randint(128, (64, 3), generator=g5)
+        other = torch.randint(128, (64, 3), generator=rdist.step_generator("cpu", 7, 6))
+        got = [torch.zeros_like(draw) for _ in range(world)]
+        dist.all_gather(got, draw)
+        ok_stream = all(torch.equal(x, draw) for x in got) and not torch.equal(draw, other)
+        q.put((rank, lo, hi, ok_mean, ok_bcast and ok_stream))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e), False, False))
