@@ -37,7 +37,7 @@ def _split_gate(flat, K):
 
 def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gate_master,
                   scale, seeds=None, bg=None, T_threshold=1e-4, log2_T=19, grid_size=128,
-                  input_grads=False):
+                  input_grads=False, gate_in2=None):
     """One fwd (+ bwd if seeds) step.  All inputs numpy / CPU tensors.
 
     input_grads: also differentiate w.r.t. rays_o / rays_d (--optimize_ext,
@@ -69,7 +69,10 @@ def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gat
     mlp_p = torch.tensor(np.asarray(mlp_master, np.float32)).requires_grad_(True)
     gate_p = torch.tensor(np.asarray(gate_master, np.float32)).requires_grad_(True)
 
-    gate = fo.gate_forward(torch.cat([o_t, d_t], 1), _split_gate(gate_p, K))
+    # gate input: cat(rays_o, rays_d), or cat(rays_o, imgs_d) for gate_type
+    # "image" (ml_rendering.py:31-36)
+    second = d_t if gate_in2 is None else torch.from_numpy(np.asarray(gate_in2, np.float32))
+    gate = fo.gate_forward(torch.cat([o_t, second], 1), _split_gate(gate_p, K))
 
     counts, starts, xyzs, ts, deltas, total = oracle.ml_march(
         rays_o, rays_d, center, half, noise, bitfields, cascades, scale, esf, grid_size,
@@ -146,3 +149,78 @@ def ml_train_step(rays_o, rays_d, bitfields, noise, grid_master, mlp_master, gat
                 "gate_grad": gate_p.grad.numpy() if gate_p.grad is not None else None,
                 "dgate": None})
     return res
+
+
+def _hits(rays_o, rays_d, scale):
+    """ml_rendering.py:48-50: AABB hits + NEAR_DISTANCE clamp, (B, 2)."""
+    c = np.zeros((1, 3), np.float32)
+    h = np.full((1, 3), scale, np.float32)
+    _, ht, _ = oracle.ray_aabb_intersect(rays_o, rays_d, c, h, 1)
+    ht = np.ascontiguousarray(ht[:, 0])
+    m = (ht[:, 0] >= 0) & (ht[:, 0] < NEAR_DISTANCE)
+    ht[m, 0] = NEAR_DISTANCE
+    return ht
+
+
+def ml_render_test(rays_o, rays_d, bitfields, grid_master, mlp_master, gate_master, scale,
+                   gate_in2=None, T_threshold=1e-4, log2_T=19, grid_size=128):
+    """ml_render(test_time=True): the gate, then per sub-NeRF the host-driven
+    progressive-compaction loop of __render_rays_test (ml_rendering.py:81-155:
+    raymarching_test with in-place hits_t, the field on the valid samples,
+    composite_test_fw, drop converged rays, N_samples = max(min(N/N_alive, 64),
+    min_samples)), background, gate-weighted combine (:41-78)."""
+    K = bitfields.shape[0]
+    B = len(rays_o)
+    cascades = max(1 + int(np.ceil(np.log2(2 * scale))), 1)
+    esf = 1.0 / 256 if scale > 0.5 else 0.0
+    lv = fo.grid_levels(scale, log2_T)
+    xyz_min = torch.full((1, 3), -float(scale))
+    xyz_max = torch.full((1, 3), float(scale))
+    o = np.ascontiguousarray(rays_o, np.float32)
+    d = np.ascontiguousarray(rays_d, np.float32)
+    second = d if gate_in2 is None else np.ascontiguousarray(gate_in2, np.float32)
+    grid_p = torch.tensor(np.asarray(grid_master, np.float32)).half().float()
+    mlp_p = torch.tensor(np.asarray(mlp_master, np.float32))
+    with torch.no_grad():
+        gate = fo.gate_forward(torch.from_numpy(np.concatenate([o, second], 1)),
+                               _split_gate(torch.tensor(np.asarray(gate_master, np.float32)), K)).numpy()
+    bg = np.ones(3, np.float32) if esf == 0 else np.zeros(3, np.float32)
+    rgb_acc = np.zeros((B, 3), np.float32)
+    op_acc = np.zeros(B, np.float32)
+    depth_all = np.zeros((B, K), np.float32)
+    min_samples = 1 if esf == 0 else 4
+    for k in range(K):
+        ht = _hits(o, d, scale)
+        opacity = np.zeros(B, np.float32)
+        depth = np.zeros(B, np.float32)
+        rgb = np.zeros((B, 3), np.float32)
+        alive = np.arange(B, dtype=np.int64)
+        samples = 0
+        while samples < MAX_SAMPLES:
+            n_alive = len(alive)
+            if n_alive == 0:
+                break
+            ns = max(min(B // n_alive, 64), min_samples)
+            samples += ns
+            xyzs, dirs, deltas, ts, n_eff = oracle.raymarching_test(
+                o, d, ht, alive, bitfields[k], cascades, scale, esf, grid_size, MAX_SAMPLES, ns)
+            xyzs = xyzs.reshape(-1, 3)
+            dirs = dirs.reshape(-1, 3)
+            valid = ~np.all(dirs == 0, axis=1)
+            if valid.sum() == 0:
+                break
+            sig = np.zeros(len(xyzs), np.float32)
+            col = np.zeros((len(xyzs), 3), np.float32)
+            with torch.no_grad():
+                s_v, c_v = fo.field_forward(torch.from_numpy(xyzs[valid]), torch.from_numpy(dirs[valid]),
+                                            grid_p, _split_field(mlp_p[k]), lv, xyz_min, xyz_max)
+            sig[valid] = s_v.numpy()
+            col[valid] = c_v.numpy()
+            oracle.composite_test_fw(sig.reshape(-1, ns), col.reshape(-1, ns, 3), deltas, ts, alive,
+                                     T_threshold, n_eff, opacity, depth, rgb)
+            alive = np.ascontiguousarray(alive[alive >= 0])
+        rgb_k = rgb + bg * (1 - opacity)[:, None]
+        rgb_acc = rgb_acc + rgb_k * gate[:, k][:, None]
+        op_acc = op_acc + opacity * gate[:, k]
+        depth_all[:, k] = depth
+    return {"rgb": rgb_acc, "opacity": op_acc, "depth": depth_all, "gate": gate}

@@ -123,3 +123,61 @@ def test_density_grid_update(cuda):
         mean = dg[dg > 0].mean().item()
         bits = oracle.packbits(grid.reshape(-1), min(float(mean), thr))
         assert np.array_equal(getattr(m, f"density_bitfield_{i}").cpu().numpy(), bits)
+
+
+@pytest.mark.parametrize("scale,K", [(0.5, 2), (16.0, 2), (16.0, 4)])
+def test_test_time_render_vs_oracle(cuda, scale, K):
+    """a10: ml_render(test_time=True) -- raymarching_test with the cascades
+    quirk of calc_dt (raymarching.cu:370,399), the host compaction loop of
+    ml_rendering.py:81-155, composite_test_fw -- vs the oracle's restatement of
+    the same loop; at scale 16 (exp step 1/256, 6 cascades) it differs from the
+    training march, so it is checked against the oracle directly."""
+    B = 600
+    m = MNGP(scale, size=K, seed=3)
+    bits = _init(m, K, p=0.3)
+    g = Ray_Gate(K, seed=2)
+    with torch.no_grad():
+        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6)[0]))
+    m, g = m.to(cuda), g.to(cuda)
+    o, d = S.rays(B, scale)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    with torch.no_grad():
+        te = ml_render(m, g, t(o), t(d), t(d), test_time=True, exp_step_factor=esf)
+    ref = ml_oracle.ml_render_test(o, d, bits, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                   m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale)
+    errs = {k: float(np.abs(te[k].float().cpu().numpy() - ref[k]).max())
+            for k in ("rgb", "opacity", "depth")}
+    print(f"test-time render scale {scale} K {K}: {errs}, opacity mean {ref['opacity'].mean():.3f}")
+    assert all(v <= 1e-4 for v in errs.values()), errs
+
+
+@pytest.mark.parametrize("scale", [0.5, 16.0])
+def test_image_gate(cuda, scale):
+    """gate_type=image (ml_rendering.py:31-36): the gate sees cat(rays_o,
+    imgs_d); fused and drop-in chains vs the oracle, outputs and gradients."""
+    from radnerf_amd.fused import ml_render_fused
+    from tests_parity_helpers import setup_ml
+    B, K = 384, 2
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = setup_ml(cuda, B, K, scale, gate_type="image")
+    imgs_d = S.rays(B, scale, seed=77)[1]
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    outs = []
+    for fn in (ml_render_fused, ml_render):
+        m.zero_grad(); g.zero_grad()
+        res = fn(m, g, to(o), to(d), to(imgs_d), noise=to(noise), exp_step_factor=esf)
+        torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]], [to(s) for s in seeds])
+        outs.append((res, g.params.grad.clone()))
+    ref = ml_oracle.ml_train_step(o, d, bits, noise, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                  m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale,
+                                  seeds=seeds, gate_in2=imgs_d)
+    for res, gg in outs:
+        assert np.abs(res["gating_code"].detach().cpu().numpy() - ref["gate"]).max() <= 1e-5
+        assert np.abs(res["rgb"].detach().cpu().numpy() - ref["rgb"]).max() <= 1e-4
+        e = float(np.linalg.norm(gg.cpu().numpy() - ref["gate_grad"]) / np.linalg.norm(ref["gate_grad"]))
+        assert e <= 2e-3, e
+    # the image gate differs from the ray gate on these inputs
+    assert np.abs(ref["gate"] - ml_oracle.ml_train_step(
+        o, d, bits, noise, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+        m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale)["gate"]).max() > 1e-3
