@@ -260,7 +260,7 @@ def main():
             model.zero_grad(set_to_none=True)
             gate.zero_grad(set_to_none=True)
             res = ml_render(model, gate, rays_o, rays_d, rays_d, noise=noises[i % 4],
-                            exp_step_factor=esf)
+                            exp_step_factor=esf, fused=False)
             torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
                                     [g_rgb, g_op, g_depth])
 

@@ -3,12 +3,13 @@
 `render(model, rays_o, rays_d, **kw)`            rendering.py:12-46 (single NGP)
 `ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kw)`
                                                   ml_rendering.py:11-78 (Rad-NeRF)
-Both keep the reference's autograd structure (RayAABBIntersector ->
-RayMarcher -> model(x, d[, i]) -> VolumeRenderer, then background and the
-gate-weighted combine) and the reference's result keys.  For training with
-model_zoo_size > 1 the fused single-pass path (radnerf_amd.fused) computes the
-same outputs with fewer launches and no host synchronisation; pass
-`fused=True` to route ml_render there.
+Both return the reference's result keys.  A training render (test_time
+False) of ml_render runs the fused single-chain path (radnerf_amd.fused): the
+same outputs and gradients (tests/test_gpu_ml.py: outputs within 1e-5,
+gradients within 1e-3) with fewer launches and no host synchronisation, 988 vs
+578 M samples/s on C3.  `fused=False` keeps the reference's op-by-op autograd
+structure (RayAABBIntersector -> RayMarcher -> model(x, d, i) ->
+VolumeRenderer per sub-NeRF, then background and the gate-weighted combine).
 
 Test-time rendering follows the host-driven compaction loop of
 ml_rendering.py:81-155 / rendering.py:113-189.
@@ -118,8 +119,12 @@ def _to_host(res, kw):
 
 
 def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):
-    """ml_rendering.py:11-78: gate, K sub-NeRF renders, gate-weighted combine."""
-    if kwargs.get("fused", False) and not kwargs.get("test_time", False):
+    """ml_rendering.py:11-78: gate, K sub-NeRF renders, gate-weighted combine.
+    fused (default: training renders) routes to radnerf_amd.fused."""
+    fused = kwargs.pop("fused", None)
+    if fused is None:
+        fused = not kwargs.get("test_time", False)
+    if fused and not kwargs.get("test_time", False):
         from .fused import ml_render_fused
         return ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup, **kwargs)
     with torch.autocast("cuda"):

@@ -11,6 +11,8 @@
        the oracle on the updated grid, and the grid holds the field's σ at the
        jittered cell positions.
 """
+import functools
+
 import numpy as np
 import pytest
 import torch
@@ -76,7 +78,7 @@ def test_test_time_render_matches_train_without_jitter(cuda, K):
     m, g = m.to(cuda), g.to(cuda)
     o, d = (torch.from_numpy(a).to(cuda) for a in S.rays(B, scale))
     with torch.no_grad():
-        tr = ml_render(m, g, o, d, d, noise=torch.zeros(K, B, device=cuda))
+        tr = ml_render(m, g, o, d, d, noise=torch.zeros(K, B, device=cuda), fused=False)
         te = ml_render(m, g, o, d, d, test_time=True)
     for k in ("rgb", "opacity", "depth"):
         err = (tr[k].float() - te[k].float()).abs().max().item()
@@ -158,13 +160,14 @@ def test_image_gate(cuda, scale):
     imgs_d); fused and drop-in chains vs the oracle, outputs and gradients."""
     from radnerf_amd.fused import ml_render_fused
     from tests_parity_helpers import setup_ml
+    dropin = functools.partial(ml_render, fused=False)
     B, K = 384, 2
     esf = 1 / 256 if scale > 0.5 else 0.0
     m, g, o, d, noise, seeds, bits = setup_ml(cuda, B, K, scale, gate_type="image")
     imgs_d = S.rays(B, scale, seed=77)[1]
     to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
     outs = []
-    for fn in (ml_render_fused, ml_render):
+    for fn in (ml_render_fused, dropin):
         m.zero_grad(); g.zero_grad()
         res = fn(m, g, to(o), to(d), to(imgs_d), noise=to(noise), exp_step_factor=esf)
         torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]], [to(s) for s in seeds])
