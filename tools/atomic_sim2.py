@@ -25,11 +25,13 @@ from radnerf_amd import synthetic as S  # noqa: E402
 
 def merged_samples(B, K=2, scale=0.5, p=0.5):
     o, d = S.rays(B, scale, seed=0)
-    bits = S.bitfields(K, 1, p=p, seed=1)
+    C = LY.cascades_for_scale(scale)
+    bits = S.bitfields(K, C, p=p, seed=1)
     nz = S.noise(K, B, seed=2)
+    esf = 1 / 256 if scale > 0.5 else 0.0
     cnt, st, xyz, ts, dl, tot = oracle.ml_march(o, d, np.zeros(3, np.float32),
-                                                np.full(3, scale, np.float32), nz, bits, 1,
-                                                scale, 0.0)
+                                                np.full(3, scale, np.float32), nz, bits, C,
+                                                scale, esf)
     ray = np.concatenate([np.repeat(np.arange(B), cnt[k]) for k in range(K)])
     mod = np.concatenate([np.full(cnt[k].sum(), k) for k in range(K)])
     order = np.lexsort((mod, ts, ray))
@@ -143,6 +145,31 @@ def requests(u, lv, sid, issue=32, levels=range(16), lane_major=False, cut_min=0
     return total / n
 
 
+def floor(u, ray, lv, ent_per_seg=8):
+    """distinct (ray, level, segment) triples per sample: every corner entry of
+    a ray's samples, all K models merged, one request per distinct segment"""
+    n = len(u)
+    total = 0
+    for l in range(16):
+        sc, res, hs, off = lv["scale"][l], int(lv["res"][l]), int(lv["hsize"][l]), int(lv["offset"][l])
+        g = np.floor(sc * u + np.float32(0.5)).astype(np.int64)
+        segs = []
+        for c in range(8):
+            X, Y, Z = g[:, 0] + (c & 1), g[:, 1] + ((c >> 1) & 1), g[:, 2] + (c >> 2)
+            if res ** 3 <= hs:
+                idx = (X + Y * res + Z * res * res) % hs
+            else:
+                idx = (X ^ ((Y * 2654435761) & 0xFFFFFFFF) ^ ((Z * 805459861) & 0xFFFFFFFF)) % hs
+            segs.append((idx + off) // ent_per_seg)
+        key = np.stack([np.repeat(ray[None], 8, 0).ravel(), np.concatenate(segs)], 1)
+        total += len(np.unique(key, axis=0))
+    return total / n
+
+
+def eps_floor(argv):
+    return int(argv[7]) if len(argv) > 7 else 8
+
+
 def main():
     B = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
     mc = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
@@ -152,7 +179,12 @@ def main():
     cut_min = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     eps = int(sys.argv[7]) if len(sys.argv) > 7 else 8
     sw = int(sys.argv[8]) if len(sys.argv) > 8 else 0
-    u, ray, lv = merged_samples(B)
+    scale = float(os.environ.get("SIM_SCALE", 0.5))
+    K = int(os.environ.get("SIM_K", 2))
+    u, ray, lv = merged_samples(B, K=K, scale=scale)
+    if os.environ.get("SIM_FLOOR"):
+        print(f"scale {scale} K {K} B {B}: floor {floor(u, ray, lv, eps_floor(sys.argv)):.2f} "
+              f"requests/sample")
     sid = streams(ray, mc, parts=parts)
     print(f"B {B} samples {len(u)} max_chunk {mc} issue {issue} parts {parts} "
           f"{'lane' if lane_major else 'slot'}-major: "
