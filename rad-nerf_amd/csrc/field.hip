@@ -1292,6 +1292,119 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
     }
 }
 
+// The same merged order for K > 2 by a merge tree in LDS: the ray's K runs
+// (staged with their sample indices) are merged pairwise, log2(K) levels; each
+// pair is merged by the whole wave with merge path (lane j: a diagonal binary
+// search, then L serial steps).  Runs are merged in model order and the left
+// run wins ties, so the result is ordered by (t, model) like k_bwd_plan's
+// ranks.  ~log2(n) + n/64 dependent LDS reads per lane and level instead of
+// (K-1) binary searches per sample (C5: K = 8, ~760 samples per ray).
+#define PLANM_WAVES 2
+#define PLANM_LDS 2048     // samples per wave
+
+__device__ __forceinline__ void merge_pair_wave(const float* tA, const int* iA, int nA,
+                                                const float* tB, const int* iB, int nB,
+                                                float* to, int* io, int32_t* gout) {
+    const int lane = rn_lane();
+    const int n = nA + nB;
+    const int L = (n + RN_WAVE - 1) / RN_WAVE;
+    const int d = min(lane * L, n);
+    int lo = max(0, d - nB), hi = min(d, nA);
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tA[mid] <= tB[d - 1 - mid]) lo = mid + 1; else hi = mid;
+    }
+    int a = lo, b = d - lo;
+    const int e = min(d + L, n);
+    for (int q = d; q < e; ++q) {
+        const bool takeA = a < nA && (b >= nB || tA[a] <= tB[b]);
+        const int idx = takeA ? iA[a] : iB[b];
+        if (gout) gout[q] = idx;
+        else { to[q] = takeA ? tA[a] : tB[b]; io[q] = idx; }
+        a += takeA ? 1 : 0;
+        b += takeA ? 0 : 1;
+    }
+}
+
+__global__ void __launch_bounds__(PLANM_WAVES * 64)
+k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
+                 const int32_t* __restrict__ offsets, const int32_t* __restrict__ seg_base,
+                 const int32_t* __restrict__ seg_count, const float* __restrict__ ts,
+                 int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
+    __shared__ float sT[PLANM_WAVES][2][PLANM_LDS];
+    __shared__ int sI[PLANM_WAVES][2][PLANM_LDS];
+    const int wid = threadIdx.x / RN_WAVE;
+    const int r = blockIdx.x * PLANM_WAVES + wid;
+    if (r >= B) return;                      // wave-uniform; no block barrier below
+    const int lane = rn_lane();
+    int ms = 0, tot_r = 0;
+    int bnd[MB_KMAX + 1], off[MB_KMAX];
+    for (int k = 0; k < K; ++k) {
+        const int c = counts[k * B + r];
+        off[k] = offsets[k * B + r];
+        ms += off[k] - seg_base[k];
+        bnd[k] = tot_r; tot_r += c;
+    }
+    bnd[K] = tot_r;
+    if (lane == 0) {
+        mstart[r] = ms;
+        if (r == 0) {
+            int tot = 0;
+            for (int k = 0; k < K; ++k) tot += seg_count[k];
+            mstart[B] = tot;
+        }
+    }
+    if (tot_r > PLANM_LDS) {
+        // (rays longer than the LDS slice: rank by binary searches in global memory)
+        for (int k = 0; k < K; ++k) {
+            const int ck = bnd[k + 1] - bnd[k];
+            for (int i = lane; i < ck; i += RN_WAVE) {
+                const float t = ts[off[k] + i];
+                int pos = i;
+                for (int k2 = 0; k2 < K; ++k2) {
+                    if (k2 == k) continue;
+                    int lo = 0, hi = bnd[k2 + 1] - bnd[k2];
+                    while (lo < hi) {
+                        const int mid = (lo + hi) >> 1;
+                        const float t2 = ts[off[k2] + mid];
+                        if (t2 < t || (k2 < k && t2 == t)) lo = mid + 1; else hi = mid;
+                    }
+                    pos += lo;
+                }
+                perm[ms + pos] = off[k] + i;
+            }
+        }
+        return;
+    }
+    int cur = 0;
+    for (int k = 0; k < K; ++k)
+        for (int i = lane; i < bnd[k + 1] - bnd[k]; i += RN_WAVE) {
+            sT[wid][0][bnd[k] + i] = ts[off[k] + i];
+            sI[wid][0][bnd[k] + i] = off[k] + i;
+        }
+    int nr = K;
+    while (true) {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        const bool last = nr <= 2;
+        const float* ts_ = sT[wid][cur];
+        const int* is_ = sI[wid][cur];
+        for (int p = 0; 2 * p < nr; ++p) {
+            const int a0 = bnd[2 * p], a1 = bnd[min(2 * p + 1, nr)], b1 = bnd[min(2 * p + 2, nr)];
+            merge_pair_wave(ts_ + a0, is_ + a0, a1 - a0, ts_ + a1, is_ + a1, b1 - a1,
+                            sT[wid][cur ^ 1] + a0, sI[wid][cur ^ 1] + a0,
+                            last ? perm + ms + a0 : nullptr);
+        }
+        if (last) return;
+        // runs after this level: boundaries of the merged pairs
+        const int nn = (nr + 1) / 2;
+        for (int p = 0; p < nn; ++p) bnd[p] = bnd[2 * p];
+        bnd[nn] = bnd[nr];
+        nr = nn;
+        cur ^= 1;
+    }
+}
+
 // Chunk schedule of the merged backward over the merged positions [0, total):
 // chunks of max_chunk positions for the first 7/8 of the work, then chunks of
 // min_chunk (a short tail: blocks finish together).  Chunk c holds the rays
@@ -1493,8 +1606,12 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                  head_size >= 0 && head_size <= max_chunk, "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
                  chunk_first && chunk_desc && queue, "null pointer");
-    k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
-        (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
+    if (n_models > 2)
+        k_bwd_plan_multi<<<nblk(n_rays, PLANM_WAVES), PLANM_WAVES * 64, 0, (hipStream_t)stream>>>(
+            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
+    else
+        k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
+            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, mstart, offsets, seg_base, seg_count, head_chunks, head_size,
