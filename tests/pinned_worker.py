@@ -26,7 +26,9 @@ def main(out_path):
     rank, _, world = rdist.init(backend="gloo")
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    B, K, scale = int(os.environ.get("PIN_RAYS", 2048)), int(os.environ.get("PIN_K", 2)), 0.5
+    B, K = int(os.environ.get("PIN_RAYS", 2048)), int(os.environ.get("PIN_K", 2))
+    scale = float(os.environ.get("PIN_SCALE", 0.5))
+    esf = 1 / 256 if scale > 0.5 else 0.0
     model = MNGP(scale, size=K, seed=3).to(dev)
     gate = Ray_Gate(K, seed=4).to(dev)
     bits = S.bitfields(K, model.cascades, p=0.5, seed=1)
@@ -36,12 +38,12 @@ def main(out_path):
     o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B, scale, seed=0))
     noise = torch.from_numpy(S.noise(K, B, seed=2)).to(dev)
     g_rgb, g_op, g_depth = (torch.from_numpy(s).to(dev) for s in S.loss_seeds(B, K, seed=4))
-    bg = torch.ones(3, device=dev)
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
 
     r = PinnedMLRenderer(model, gate, B)
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     ar.zero()
-    rgb, op, depth, g_out, imp = r.forward(o, d, d, noise, bg, 1e-4, 0.0)
+    rgb, op, depth, g_out, imp = r.forward(o, d, d, noise, bg, 1e-4, esf)
     n = r.ws.meta[1].to(torch.int64).clone()
     r.backward(o, d, d, g_out, bg, g_rgb, g_op, g_depth, None, 1e-4,
                grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
@@ -50,7 +52,7 @@ def main(out_path):
     torch.cuda.synchronize()
     if rank == 0:
         ref = FusedMLRenderer(model, gate, B)
-        rgb_r, op_r, depth_r, g_r, _ = ref.forward(o, d, d, noise, bg, 1e-4, 0.0)
+        rgb_r, op_r, depth_r, g_r, _ = ref.forward(o, d, d, noise, bg, 1e-4, esf)
         gg, mg, ag = ref.backward(o, d, d, g_r, bg, g_rgb, g_op, g_depth, None, 1e-4)
         torch.cuda.synchronize()
         res = {"world": world, "samples": int(n), "samples_ref": int(ref.ws.meta[1]),

@@ -60,9 +60,11 @@ def _port():
     return p
 
 
-def test_pinned_two_ranks_one_gpu(tmp_path):
-    """2 ranks (one sub-NeRF each) on one GPU over gloo: the all-gather of the
-    per-ray outputs and the summed all-reduce reproduce the K = 2 result."""
+@pytest.mark.parametrize("K,rays,scale", [(2, 2048, 0.5), (8, 1024, 16.0)])
+def test_pinned_two_ranks_one_gpu(tmp_path, K, rays, scale):
+    """2 ranks on one GPU over gloo (K/2 sub-NeRFs each; (8, 1024, 16) is config
+    C5's layout: K = 8, scale 16, exp step): the all-gather of the per-ray
+    outputs and the summed all-reduce reproduce the single-process result."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     out = tmp_path / "pinned.json"
@@ -70,7 +72,8 @@ def test_pinned_two_ranks_one_gpu(tmp_path):
     procs = []
     for rank in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                   LOCAL_RANK=str(rank), WORLD_SIZE="2", PIN_K="2", PIN_RAYS="2048")
+                   LOCAL_RANK=str(rank), WORLD_SIZE="2", PIN_K=str(K), PIN_RAYS=str(rays),
+                   PIN_SCALE=str(scale))
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "pinned_worker.py"),
                                        str(out)], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
