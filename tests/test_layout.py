@@ -71,3 +71,26 @@ def test_kperm_accumulator_identity():
             for j in range(8):
                 i = 8 * s + j
                 assert LY._perm(s, h, j) == (i & 3) + 8 * (i >> 2) + 4 * h
+
+
+def test_dinput_fragment_tables():
+    """Input-gradient fragments: the rgb net's SH columns Wr1[:, 0:16]^T (rows =
+    SH inputs, k = 64 hidden) -- exactly the entries the backward transposes
+    omit -- and the gate's W0^T (rows = the 6 inputs)."""
+    fi = LY.field_dinput_frag_index()
+    assert fi.shape == (4 * 512,)
+    sl = LY.split_field_params(np.arange(LY.FIELD_PARAMS))
+    v = fi[fi >= 0]
+    assert sorted(v.tolist()) == sorted(sl["r1"][:, :16].reshape(-1).tolist())
+    # slot (frag q, lane l, elem j): row r = l & 31 (SH input), k = _kin(q, h, j) (hidden)
+    for q in range(4):
+        for l in (0, 5, 37, 63):
+            r, h = l & 31, l >> 5
+            for j in range(8):
+                want = sl["r1"][LY._kin(q, h, j), r] if r < 16 else -1
+                assert fi[q * 512 + l * 8 + j] == want
+    for K in (2, 8):
+        gi = LY.gate_dinput_frag_index(K)
+        sg = LY.split_gate_params(np.arange(LY.gate_params(K)), K)
+        v = gi[gi >= 0]
+        assert sorted(v.tolist()) == sorted(sg["w0"].reshape(-1).tolist())
