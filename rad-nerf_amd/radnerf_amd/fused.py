@@ -376,6 +376,8 @@ class FusedMLRenderer:
 
         gate_dx = self._gate_dinput(B, dev) if self.input_grad else None
         gate_dfr = g.packed_dinput_frags() if gate_dx is not None and G > 1 else None
+        if gate_dx is not None and not self.gate_grad_here:
+            gate_dx.zero_()             # no gate backward on this process
 
         def gate_bwd(stream):
             if G == 1:              # d softmax over one model = 0: nothing to add

@@ -126,6 +126,11 @@ class PinnedMLRenderer(FusedMLRenderer):
                  dL_dgate_ext=None, T_threshold=1e-4, grid_grad=None, mlp_grad=None,
                  gate_grad=None):
         """mlp_grad: the full (K, FIELD_PARAMS) buffer; this rank adds its rows."""
+        if self.input_grad:
+            # each rank would hold the ray gradients of its own sub-NeRFs only
+            raise NotImplementedError(
+                "PinnedMLRenderer: gradients into rays_o / rays_d (--optimize_ext) are not "
+                "supported in the sub-NeRF-per-GPU layout; use the data-parallel renderer")
         m = self.full_model
         grid_grad = torch.zeros_like(m.xyz_encoder.params) if grid_grad is None else grid_grad
         mlp_grad = torch.zeros_like(m.mlp_params) if mlp_grad is None else mlp_grad
