@@ -74,6 +74,8 @@ def parse():
                     help="also time the full train step (loss + Adam); 0 = skip")
     ap.add_argument("--dropin-step", type=int, default=1,
                     help="also time the step through the drop-in rendering.ml_render chain; 0 = skip")
+    ap.add_argument("--test-time-rays", type=int, default=640000,
+                    help="rays of the test-time render leg (one 800x800 image; 0 = skip)")
     ap.add_argument("--density-update", type=int, default=1,
                     help="also time the occupancy-grid update (warm-up and sampled); 0 = skip")
     ap.add_argument("--split-bwd", action="store_true",
@@ -301,6 +303,26 @@ def main():
         cells = model.cascades * 128 ** 3
         density = {"ms": dms, "cells_per_model_warmup": cells, "models": K,
                    "kernel": "rn_field_density (hash grid + geo MLP) + morton / packbits"}
+    # test-time render (row a10, ml_rendering.py:81-155): one image of
+    # --test-time-rays rays through ml_render(test_time=True); not part of `value`
+    test_time = None
+    if args.test_time_rays and world == 1:
+        from radnerf_amd.rendering import ml_render
+        nt = args.test_time_rays
+        ot, dt_ = (torch.from_numpy(a).to(dev) for a in S.rays(nt, scale, seed=99))
+        with torch.no_grad():
+            res_t = ml_render(model, gate, ot, dt_, dt_, test_time=True, exp_step_factor=esf)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps = 3
+            for _ in range(reps):
+                res_t = ml_render(model, gate, ot, dt_, dt_, test_time=True, exp_step_factor=esf)
+            torch.cuda.synchronize()
+            t_el = (time.perf_counter() - t0) / reps
+        test_time = {"rays": nt, "ms_per_image": round(t_el * 1e3, 3),
+                     "Mrays_per_s": round(nt / t_el / 1e6, 3),
+                     "opacity_mean": round(float(res_t["opacity"].mean()), 4),
+                     "path": "rendering.ml_render(test_time=True): host compaction loop"}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:
@@ -383,6 +405,7 @@ def main():
                "train_step": train,
                "dropin_step": dropin,
                "density_update": density,
+               "test_time_render": test_time,
                # MFMA use: algorithmic MLP flops (56,832 per sample
                # fwd+bwd, unpadded) at `value`, against the dense f16 peak
                "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),
