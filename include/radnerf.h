@@ -225,7 +225,30 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
                         int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
-                        void* stream);
+                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_vmax,
+                        const int32_t* fx_redo, int32_t fx_mode, void* stream);
+
+/* Fixed-point accumulation of the hashed levels' grid gradient (fx_mode 2,
+ * the fused renderer's default; needs the encoding cache).  fx_acc: int32, one
+ * per grid_grad element, zero on entry; fx_scale [16] f32 per level: 2^e_l, or
+ * 0 for fp32 atomics into grid_grad (dense levels, first step); fx_vmax [16]
+ * u32: the kernel atomic-maxes the bits of each level's largest |record|.
+ * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
+ * memory side serves them ~27 % faster than f32 adds), so those levels'
+ * gradients are order-independent and bitwise reproducible.
+ * rn_grid_fx_fold then (1) sets *fx_redo when a level's largest record reached
+ * 2^22 units or was not finite, writes the next step's scales
+ * (2^(19 - e), |record| < 2^e; dense levels 0) to fx_scale_next and clears
+ * fx_vmax, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
+ * and re-zeroes fx_acc.  The caller then launches rn_field_bwd_merged with
+ * fx_mode 3 and the same fx_scale (fp32 redo of the fixed-point levels' grid
+ * scatter, no dW): it returns at once unless *fx_redo is set; and swaps
+ * fx_scale_cur / fx_scale_next for the next step.
+ * fx_mode 0: fp32 atomics (and the optional igrad_* integer mode).          */
+int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
+                    const uint32_t* level_res, int32_t* fx_acc, const float* fx_scale_cur,
+                    float* fx_scale_next, uint32_t* fx_vmax, int32_t* fx_redo, float* grid_grad,
+                    void* stream);
 
 /* Exact integer accumulation of the merged backward's grid gradient
  * (optional; igrad_lo == NULL keeps fp32 atomics into grid_grad).  With

@@ -285,6 +285,11 @@ struct Walk2 {
     // integer mode: the two newest issues, checked for carries one issue late
     int32_t oldA, loA, hiA, oldB, loB, hiB;
     uint32_t offA, offB;
+    // fixed-point mode (GM 2): the scales of the wave's two levels (even
+    // streams: level wid, odd: 15 - wid; 0 = fp32 atomics for that level) and
+    // the largest |record| issued for each, as float bits (NaN/inf included)
+    float fxA, fxB;
+    uint32_t vmA, vmB;
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
@@ -307,6 +312,7 @@ struct IntGrad {
     float scale;                        // 2^scale_exp (loaded from scale_ptr)
     int32_t* lo_ptr; int32_t* carry_ptr; const float* scale_ptr;
     uint32_t bytes;
+    __amdgpu_buffer_rsrc_t fx;          // fixed-point mode (GM 2): FxGrad::acc
 };
 
 __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, uint32_t off,
@@ -317,17 +323,39 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
     if (c != 0) __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(c, G.carry, (int)off, 0, 0);
 }
 
+// Fixed-point accumulation of the hashed levels' grid gradient (GM 2, the
+// default of the merged backward).  A record v of level l is added as the
+// int32 rint(v * 2^e_l) with a NON-returning u32 atomic into `acc` (same
+// layout as grid_grad): the memory side serves u32 adds at 26.6 G requests/s
+// against 20.9 for f32 (profiles/r01/atomic_probe.json), and the sums are
+// exact, so these levels' gradients are bitwise reproducible.  e_l comes from
+// the previous step's largest record of the level (rn_grid_fx_fold): that
+// record maps to < 2^19 units, leaving 2^12 max-size records of headroom per
+// entry (an entry of a hashed level takes ~77 records per C3 step, of mixed
+// sign).  The kernel records this step's largest |record| per level; when it
+// exceeds 2^22 units (8x growth) or is not finite, rn_grid_fx_fold discards
+// the fixed-point sums and the GM 3 launch redoes the grid scatter in fp32.
+// Dense levels (few requests: merged per ray) and the first step (scale 0)
+// use fp32 atomics.
+struct FxGrad {
+    int32_t* acc;              // int32 [entries][2]
+    const float* scale;        // [RN_L] 2^e_l, 0 = fp32 atomics for the level
+    uint32_t* vmax;            // [RN_L] largest |record| this step (float bits, atomicMax)
+    const int32_t* redo;       // GM 3: the launch runs only when *redo != 0
+    __amdgpu_buffer_rsrc_t rs; // over acc (built in the kernel)
+};
+
 __device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? v - W2_RING : v; }
 
 // issue up to 32 records of stream s (wave-uniform) as one atomic instruction
-template <bool IG>
+template <int GM>
 __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
     const int lane = rn_lane();
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
     asm volatile("" ::: "memory");
-    if (IG) {
+    if (GM == 1) {
         // the issue two back has had a whole issue's time to return
         ig_check(W.oldA, W.loA, W.hiA, W.offA, G);
         W.oldA = W.oldB; W.loA = W.loB; W.hiA = W.hiB; W.offA = W.offB;
@@ -340,7 +368,21 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
         if (dbg & 1) {
             asm volatile("" :: "v"(off), "v"(v));
-        } else if (IG) {
+        } else if (GM == 3 && ((s & 1) ? W.fxB : W.fxA) == 0.f) {
+            // redo: this level went in with fp32 atomics in the first pass
+        } else if (dbg & 64) {      // ablation: non-returning i32 adds (timing only)
+            (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
+                (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
+        } else if (GM == 2 && ((s & 1) ? W.fxB : W.fxA) != 0.f) {
+            const float sc = (s & 1) ? W.fxB : W.fxA;
+            const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
+            if (s & 1) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
+            // 2^e_l is a power of two: v * sc is exact; saturate (out-of-range
+            // records are caught by vmax and redone in fp32)
+            const float x = fminf(fmaxf(rintf(__uint_as_float(v) * sc), -2147483520.f),
+                                  2147483520.f);
+            (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)x, G.fx, (int)off, 0, 0);
+        } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
             const long long q = (long long)x;
@@ -350,6 +392,10 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             W.offB = off;
             W.oldB = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(lo, G.lo, (int)off, 0, 0);
         } else {
+            if (GM == 2) {                               // fp32 level: still tracked
+                const uint32_t ab = v & 0x7fffffffu;
+                if (s & 1) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
+            }
             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
                                                             (int)off, 0, 0);
         }
@@ -366,7 +412,7 @@ __device__ __forceinline__ void walk2_settle(Walk2& W, const IntGrad& G) {
 }
 
 // issue every stream with >= min_cnt pending (min_cnt 0: drain all)
-template <bool IG>
+template <int GM>
 __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
@@ -378,7 +424,7 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
         while (m) {
             const int s = __builtin_ctzll(m) >> 2;
             const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
-            walk2_issue<IG>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
+            walk2_issue<GM>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
             m &= m - 1;
         }
         if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
@@ -425,7 +471,7 @@ __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& 
 
 // walk one window: eighth e's samples are rows [32e, 32e + ne) of sG/sU
 // (ne per lane: its eighth's count; n0 = the largest, wave-uniform)
-template <bool IG>
+template <int GM>
 __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT,
                                              const float* sG_, const float* sU_, int ne, int n0,
                                              __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
@@ -482,20 +528,20 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
             W.cur1 = (dd1 & dm) | ((X1 ^ hb) & (lc.hs - 1u) & ~dm);
             W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
         }
-        walk2_drain<IG>(W, 32u, grad_rs, G, dbg);
+        walk2_drain<GM>(W, 32u, grad_rs, G, dbg);
     }
 }
 
 // end of a chunk: emit every live entry and drain the rings completely
-template <bool IG>
+template <int GM>
 __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
                                           __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                           Walk2& W, int dbg) {
     const LvConst lc = walk2_level(a, sT);
     const uint64_t smask = 0xfull << (4 * (rn_lane() >> 2));
     walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, smask, lc.off);
-    walk2_drain<IG>(W, 0u, grad_rs, G, dbg);
-    if (IG) walk2_settle(W, G);
+    walk2_drain<GM>(W, 0u, grad_rs, G, dbg);
+    if (GM == 1) walk2_settle(W, G);
     walk2_begin(W, W.ring);
 }
 
@@ -848,14 +894,21 @@ __device__ __forceinline__ void dw_unpark(const float* p, f32x16& A, f32x16& B) 
     }
 }
 
-template <int CACHE, bool ABL, bool IG>
+// GM: grid-gradient accumulation. 0 fp32 atomics, 1 exact integer with
+// carries (IntGrad), 2 fixed point for the hashed levels (FxGrad), 3 the
+// fp32 redo of a fixed-point step whose records overflowed the scale (grid
+// scatter of the levels that went in as fixed point only, no dW; the launch
+// exits at once unless *F.redo is set).
+template <int CACHE, bool ABL, int GM>
 __global__ void __launch_bounds__(BWD_WAVES * 64)
-k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
-    if (IG) {
+k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
+    if (GM == 3 && __builtin_nontemporal_load(F.redo) == 0) return;   // uniform: whole grid exits
+    if (GM == 1) {
         G.scale = *G.scale_ptr;
         G.lo = rn_rsrc(G.lo_ptr, G.bytes);
         G.carry = rn_rsrc(G.carry_ptr, G.bytes);
     }
+    if (GM == 2) G.fx = rn_rsrc(F.acc, 2 * a.grid_bytes);
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[2 * BWD_WAVES];
@@ -874,7 +927,11 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
     rn_half* imgX = imgY + RN_IMG_HALFS;
     const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
     const int dbg = ABL ? a.dbg : 0;      // ablation flags (tools/ablate.py) only in ABL builds
-    const bool do_dw = !(dbg & 2);
+    const bool do_dw = !(dbg & 2) && GM != 3;
+    // fixed point: this wave's two levels' scales (wave-uniform) and maxima
+    float fxA = 0.f, fxB = 0.f;
+    uint32_t vmA = 0u, vmB = 0u;
+    if (GM >= 2) { fxA = F.scale[wid]; fxB = F.scale[RN_L - 1 - wid]; }
     const bool do_sc = !(dbg & 4);
     float* sG = reinterpret_cast<float*>(sImg);
     float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;
@@ -985,6 +1042,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
         const int elen_lane = max(0, min(E, n_p - (rn_lane() >> 3) * E));   // walk eighth
         Walk2 W;
         walk2_begin(W, ring2);
+        W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB;
         for (int w0 = 0; w0 < E; w0 += 32) {
             const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
             const int e = j >> 5, jj = j & 31;
@@ -1019,12 +1077,21 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G) {
             if (__syncthreads_or(nz) && !(dbg & 32)) {
                 const int ne = max(0, min(32, elen_lane - w0));
                 const int n0 = max(0, min(32, min(E, n_p) - w0));
-                walk2_window<IG>(a, sT, sG, sU, ne, n0, grad_rs, G, W, dbg);
+                walk2_window<GM>(a, sT, sG, sU, ne, n0, grad_rs, G, W, dbg);
             }
             __syncthreads();
         }
-        walk2_end<IG>(a, sT, grad_rs, G, W, dbg);
+        walk2_end<GM>(a, sT, grad_rs, G, W, dbg);
+        vmA = W.vmA; vmB = W.vmB;
         __syncthreads();                         // rings (image region) drained
+    }
+    if (GM == 2) {                               // this step's largest |record| per level
+        vmA = rn_wave_max_u32(vmA);
+        vmB = rn_wave_max_u32(vmB);
+        if (rn_lane() == 0) {
+            if (vmA) atomicMax(F.vmax + wid, vmA);
+            if (vmB) atomicMax(F.vmax + RN_L - 1 - wid, vmB);
+        }
     }
     // ---- flush every model's dW (the current one from registers)
     if (do_dw) {
@@ -1204,6 +1271,78 @@ k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
     grad[i] += (float)v;
     lo[i] = 0;
     carry[i] = 0;
+}
+
+// Fixed-point step bookkeeping (one wave): redo flag of this step, the next
+// step's per-level scales from this step's largest records, vmax reset.
+// Scale 2^(19 - e) with |record| < 2^e: the largest record maps to < 2^19
+// units.  A level whose largest record reached 2^22 units under the current
+// scale (8x growth since the step the scale came from), or a non-finite one,
+// sets the redo flag: rn_grid_fx_fold then discards the fixed-point sums and
+// the GM 3 launch recomputes the grid gradient in fp32.
+__global__ void __launch_bounds__(64)
+k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
+           float* __restrict__ scale_next, uint32_t* __restrict__ vmax,
+           int32_t* __restrict__ redo) {
+    const int l = threadIdx.x;
+    bool bad = false;
+    if (l < RN_L) {
+        const uint32_t vb = vmax[l];
+        const float sc = scale_cur[l];
+        float nx = sc;                                   // no records this step: keep
+        if (vb >= 0x7f800000u) {                         // inf / NaN record
+            nx = 0.f;
+            bad = sc != 0.f;
+        } else if (vb != 0u) {
+            const float v = __uint_as_float(vb);
+            bad = sc != 0.f && v * sc >= 4194304.f;      // 2^22 units
+            int e;
+            frexpf(v, &e);                               // v < 2^e
+            nx = scalbnf(1.0f, max(-126, min(126, 19 - e)));
+        }
+        if (!((hashed_mask >> l) & 1u)) nx = 0.f;       // dense levels: fp32 atomics
+        scale_next[l] = nx;
+        vmax[l] = 0u;
+    }
+    const uint64_t b = __builtin_amdgcn_ballot_w64(bad);
+    if (l == 0) *redo = b ? 1 : 0;
+}
+
+// grid_grad += acc * 2^-e_l over the hashed levels' entries (elements
+// [e0, e1), 16-B aligned), acc = 0; with the redo flag set the sums are only
+// cleared (the fp32 redo adds the step's gradient instead).
+__global__ void __launch_bounds__(256)
+k_fx_fold(int64_t e0, int64_t e1, GridMeta gm, const float* __restrict__ scale,
+          int32_t* __restrict__ acc, float* __restrict__ grad, const int32_t* __restrict__ redo) {
+    __shared__ uint32_t sOff[RN_L];
+    __shared__ float sInv[RN_L];
+    if (threadIdx.x < RN_L) {
+        sOff[threadIdx.x] = gm.offset[threadIdx.x];
+        const float sc = scale[threadIdx.x];
+        sInv[threadIdx.x] = sc != 0.f ? 1.0f / sc : 0.f;     // exact: powers of two
+    }
+    __syncthreads();
+    const bool discard = *redo != 0;
+    const int64_t n4 = (e1 - e0) >> 2;
+    typedef int vi4 __attribute__((ext_vector_type(4)));
+    vi4* a4 = reinterpret_cast<vi4*>(acc + e0);
+    float4* g4 = reinterpret_cast<float4*>(grad + e0);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const vi4 v = __builtin_nontemporal_load(a4 + i);
+        if ((v.x | v.y | v.z | v.w) == 0) continue;
+        __builtin_nontemporal_store(vi4{0, 0, 0, 0}, a4 + i);
+        if (discard) continue;
+        const uint32_t ent = (uint32_t)((e0 + 4 * i) >> 1);
+        int l = 0;
+#pragma unroll
+        for (int k = 1; k < RN_L; ++k) l = ent >= sOff[k] ? k : l;
+        const float inv = sInv[l];
+        float4 g = g4[i];
+        g.x += (float)v.x * inv; g.y += (float)v.y * inv;
+        g.z += (float)v.z * inv; g.w += (float)v.w * inv;
+        g4[i] = g;
+    }
 }
 
 // Merged order of the K models' samples per ray (ray-major, then t, ties by
@@ -1632,8 +1771,15 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
                         int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
-                        void* stream) {
+                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_vmax,
+                        const int32_t* fx_redo, int32_t fx_mode, void* stream) {
     RN_CHECK_ARG(!igrad_lo || (igrad_carry && igrad_scale), "integer mode needs carry and scale");
+    RN_CHECK_ARG(fx_mode == 0 || fx_mode == 2 || fx_mode == 3, "fx_mode: 0, 2 or 3");
+    RN_CHECK_ARG(fx_mode != 2 || (fx_acc && fx_scale && fx_vmax && feat_cache),
+                 "fixed-point mode needs acc, scale, vmax and the encoding cache");
+    RN_CHECK_ARG(fx_mode != 3 || (fx_redo && fx_scale && feat_cache),
+                 "fixed-point redo needs the redo flag, the step's scales and the encoding cache");
+    RN_CHECK_ARG(!(igrad_lo && fx_mode), "integer and fixed-point modes are exclusive");
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX && blocks >= 1 &&
                  max_samples >= 1 && max_chunk >= 1, "bad sizes");
     RN_CHECK_ARG(scratch_rows >= (int64_t)max_chunk + (int64_t)n_models * max_samples,
@@ -1666,16 +1812,22 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         G.bytes = 2 * a.grid_bytes;            // int32 arrays, same size as the f32 grad
         G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
     }
+    FxGrad F{};
+    F.acc = fx_acc; F.scale = fx_scale; F.vmax = fx_vmax; F.redo = fx_redo;
     const dim3 blk(BWD_WAVES * 64);
-    if (igrad_lo) {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, true><<<blocks, blk, 0, st>>>(a, m, G);
-        else k_field_bwd_merged<CACHE_NONE, false, true><<<blocks, blk, 0, st>>>(a, m, G);
+    if (fx_mode == 2) {
+        k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (fx_mode == 3) {
+        k_field_bwd_merged<CACHE_READ, false, 3><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (igrad_lo) {
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, 1><<<blocks, blk, 0, st>>>(a, m, G, F);
+        else k_field_bwd_merged<CACHE_NONE, false, 1><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (a.dbg) {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, true, false><<<blocks, blk, 0, st>>>(a, m, G);
-        else k_field_bwd_merged<CACHE_NONE, true, false><<<blocks, blk, 0, st>>>(a, m, G);
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
+        else k_field_bwd_merged<CACHE_NONE, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, false><<<blocks, blk, 0, st>>>(a, m, G);
-        else k_field_bwd_merged<CACHE_NONE, false, false><<<blocks, blk, 0, st>>>(a, m, G);
+        if (feat_cache) k_field_bwd_merged<CACHE_READ, false, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
+        else k_field_bwd_merged<CACHE_NONE, false, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
     }
     RN_CHECK_LAUNCH();
     return 0;
@@ -1745,6 +1897,41 @@ int rn_seed_scale(const int32_t* seg_base, const int32_t* seg_count, int32_t n_m
     RN_CHECK_LAUNCH();
     k_seed_scale<<<1, 1, 0, st>>>(work, scale);
     RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
+                    const uint32_t* level_res, int32_t* fx_acc, const float* fx_scale_cur,
+                    float* fx_scale_next, uint32_t* fx_vmax, int32_t* fx_redo, float* grid_grad,
+                    void* stream) {
+    RN_CHECK_ARG(level_offset && level_hsize && level_res && fx_acc && fx_scale_cur &&
+                 fx_scale_next && fx_vmax && fx_redo && grid_grad, "null pointer");
+    RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
+    GridMeta gm{};
+    uint32_t hashed = 0;
+    int first = RN_L;
+    for (int l = 0; l < RN_L; ++l) {
+        gm.offset[l] = level_offset[l]; gm.hsize[l] = level_hsize[l]; gm.res[l] = level_res[l];
+        const uint64_t r = level_res[l];
+        if (r * r * r > (uint64_t)level_hsize[l]) {
+            hashed |= 1u << l;
+            first = l < first ? l : first;
+        }
+        RN_CHECK_ARG(level_offset[l] % 8 == 0, "level offsets must be multiples of 8 entries");
+    }
+    hipStream_t st = (hipStream_t)stream;
+    k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, fx_vmax, fx_redo);
+    RN_CHECK_LAUNCH();
+    if (first < RN_L) {
+        const int64_t e0 = 2 * (int64_t)level_offset[first];
+        const int64_t e1 = 2 * ((int64_t)level_offset[RN_L - 1] + level_hsize[RN_L - 1]);
+        RN_CHECK_ARG(e1 % 4 == 0, "table size must be a multiple of 2 entries");
+        const int64_t n4 = (e1 - e0) / 4;
+        const int nb = (int)std::min<int64_t>(2048, (n4 + 255) / 256);
+        k_fx_fold<<<nb > 0 ? nb : 1, 256, 0, st>>>(e0, e1, gm, fx_scale_cur, fx_acc, grid_grad,
+                                                    fx_redo);
+        RN_CHECK_LAUNCH();
+    }
     return 0;
 }
 

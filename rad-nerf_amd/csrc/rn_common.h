@@ -102,6 +102,12 @@ __device__ __forceinline__ float rn_wave_max(float v) {
     return v;
 }
 
+__device__ __forceinline__ uint32_t rn_wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off));
+    return v;
+}
+
 __device__ __forceinline__ float rn_wave_sum(float v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);

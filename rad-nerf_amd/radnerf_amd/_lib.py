@@ -51,7 +51,9 @@ SIGNATURES = {
                      I32, P],
     "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
-                            P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P],
+                            P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P, P, P,
+                            P, I32, P],
+    "rn_grid_fx_fold": [P, P, P, P, P, P, P, P, P, P],
     "rn_seed_scale": [P, P, I32, P, P, P, P, P, P],
     "rn_igrad_to_f32": [I64, P, P, P, P, P],
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,

@@ -76,6 +76,18 @@ class Workspace:
             self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
         return cap, self._chunks
 
+    def fx_buffers(self, n, device):
+        """Fixed-point grid-gradient state (rn_grid_fx_fold): int32 sums (n,
+        zero between steps), per-level scales (2, 16) (current / next, swapped
+        by fx_i each step; zeros = fp32 until the first step has measured the
+        records), per-level record maxima (16,) and the redo flag."""
+        if getattr(self, "_fx", None) is None or self._fx[0].numel() != n:
+            z = dict(device=device, dtype=torch.int32)
+            self._fx = (torch.zeros(n, **z), torch.zeros(2, 16, device=device),
+                        torch.zeros(16, **z), torch.zeros(1, **z))
+            self.fx_i = 0
+        return self._fx
+
     def bwd_scratch(self, blocks, max_chunk, max_samples=MAX_SAMPLES):
         """Per-block row scratch and dW park area of rn_field_bwd_merged."""
         rows = max_chunk + self.K * max_samples
@@ -156,6 +168,12 @@ class FusedMLRenderer:
         # one's return (the compiler's vmcnt(0)): 4.33 vs 3.81 ms on C3, so the
         # default stays fp32 atomics
         self.int_grad = False
+        # fixed-point accumulation of the hashed levels' grid gradient (u32
+        # adds, scale from the previous step's largest record, fp32 redo on
+        # overflow; rn_grid_fx_fold): field_bwd C3 3.76 -> 3.50 ms, C4 per
+        # GPU 3.29 -> 2.60, C5 10.54 -> 8.59 (tools/ablate.py, r02).  The
+        # first backward of a workspace runs fp32 (no scale yet).
+        self.grid_fx = True
         self.min_chunk = 512
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
@@ -323,6 +341,12 @@ class FusedMLRenderer:
                 self._plan(st)      # chunk sizes changed since the forward
             chunks = self._chunks
             ig = (None, None, None)
+            fx = (None, None, None, None, 0)
+            use_fx = self.grid_fx and self.feat_cache and not self.int_grad
+            if use_fx:
+                acc, scales, vmax, redo = w.fx_buffers(grid_grad.numel(), grid_grad.device)
+                cur, nxt = scales[w.fx_i], scales[1 - w.fx_i]
+                fx = (acc.data_ptr(), cur.data_ptr(), vmax.data_ptr(), None, 2)
             if self.int_grad:
                 n_g = grid_grad.numel()
                 if getattr(w, "_igrad", None) is None or w._igrad[0].numel() != n_g:
@@ -343,7 +367,23 @@ class FusedMLRenderer:
                      *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
                      dw.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
                      scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
-                     self.merged_blocks, *ig, st)
+                     self.merged_blocks, *ig, *fx, st)
+            if use_fx:
+                # fold the fixed-point sums into grid_grad (or flag the step for
+                # the fp32 redo), next step's scales; the redo launch exits at
+                # once unless flagged (no host synchronisation either way)
+                self._ev("fx_fold", L.grid_fx_fold, lo, lh, lr, acc.data_ptr(), cur.data_ptr(),
+                         nxt.data_ptr(), vmax.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(), st)
+                self._ev("fx_redo", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
+                         rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
+                         w.seg_count.data_ptr(), w.mstart.data_ptr(),
+                         w.perm.data_ptr(), w._chunk_desc.data_ptr(), w.queue.data_ptr(), w.B,
+                         m.size, MAX_SAMPLES, *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(),
+                         grid_grad.data_ptr(), dw.data_ptr(), w.feat.data_ptr(),
+                         scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
+                         self.merged_blocks, None, None, None, None, cur.data_ptr(), None,
+                         redo.data_ptr(), 3, st)
+                w.fx_i ^= 1
             if self.int_grad:
                 self._ev("igrad_to_f32", L.igrad_to_f32, grid_grad.numel(), ig[0], ig[1], ig[2],
                          grid_grad.data_ptr(), st)

@@ -22,19 +22,23 @@ from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 def main():
     flags = sys.argv[1:] or ["0", "1", "2", "4", "6"]
     dev = torch.device("cuda")
-    B, K = 8192, 2
-    m = MNGP(0.5, size=K, seed=3).to(dev)
+    # workload from the environment (default: the C3 headline)
+    B = int(os.environ.get("ABL_RAYS", 8192))
+    K = int(os.environ.get("ABL_K", 2))
+    scale = float(os.environ.get("ABL_SCALE", 0.5))
+    esf = 1.0 / 256 if scale > 0.5 else 0.0
+    m = MNGP(scale, size=K, seed=3).to(dev)
     g = Ray_Gate(K, seed=4).to(dev)
-    bits = S.bitfields(K, 1, p=0.5)
+    bits = S.bitfields(K, m.cascades, p=0.5)
     with torch.no_grad():
         for i in range(K):
             getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
-    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B))
+    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B, scale))
     nz = torch.from_numpy(S.noise(K, B)).to(dev)
     sd = [torch.from_numpy(a).to(dev) for a in S.loss_seeds(B, K)]
-    bg = torch.ones(3, device=dev)
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
     r = FusedMLRenderer(m, g, B)
-    _, _, _, gt, _ = r.forward(o, d, d, nz, bg)
+    _, _, _, gt, _ = r.forward(o, d, d, nz, bg, 1e-4, esf)
     gg = torch.zeros_like(m.xyz_encoder.params)
     mg = torch.zeros_like(m.mlp_params)
     ag = torch.zeros_like(g.params)
