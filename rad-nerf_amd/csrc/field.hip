@@ -354,6 +354,9 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                                             int dbg) {
     const int lane = rn_lane();
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
+    // the stream's level: even streams level wid, odd 15 - wid (scalar)
+    const bool odd = s & 1;
+    const float sc_s = GM >= 2 ? (odd ? W.fxB : W.fxA) : 0.f;
     asm volatile("" ::: "memory");
     if (GM == 1) {
         // the issue two back has had a whole issue's time to return
@@ -368,20 +371,20 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
         if (dbg & 1) {
             asm volatile("" :: "v"(off), "v"(v));
-        } else if (GM == 3 && ((s & 1) ? W.fxB : W.fxA) == 0.f) {
+        } else if (GM == 3 && sc_s == 0.f) {
             // redo: this level went in with fp32 atomics in the first pass
         } else if (dbg & 64) {      // ablation: non-returning i32 adds (timing only)
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
                 (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
-        } else if (GM == 2 && ((s & 1) ? W.fxB : W.fxA) != 0.f) {
-            const float sc = (s & 1) ? W.fxB : W.fxA;
+        } else if (GM == 2 && sc_s != 0.f) {
             const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
-            if (s & 1) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
-            // 2^e_l is a power of two: v * sc is exact; saturate (out-of-range
-            // records are caught by vmax and redone in fp32)
-            const float x = fminf(fmaxf(rintf(__uint_as_float(v) * sc), -2147483520.f),
-                                  2147483520.f);
-            (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32((int)x, G.fx, (int)off, 0, 0);
+            if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
+            // 2^e_l is a power of two: v * sc is exact; v_cvt_i32_f32 saturates
+            // out-of-range values (NaN -> 0): such records are caught by vmax
+            // and the step is redone in fp32
+            int q;
+            asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
+            (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -394,7 +397,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         } else {
             if (GM == 2) {                               // fp32 level: still tracked
                 const uint32_t ab = v & 0x7fffffffu;
-                if (s & 1) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
+                if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             }
             __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
                                                             (int)off, 0, 0);
@@ -931,7 +934,10 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     // fixed point: this wave's two levels' scales (wave-uniform) and maxima
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
-    if (GM >= 2) { fxA = F.scale[wid]; fxB = F.scale[RN_L - 1 - wid]; }
+    if (GM >= 2) {
+        fxA = __builtin_amdgcn_readfirstlane(F.scale[wid]);
+        fxB = __builtin_amdgcn_readfirstlane(F.scale[RN_L - 1 - wid]);
+    }
     const bool do_sc = !(dbg & 4);
     float* sG = reinterpret_cast<float*>(sImg);
     float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;

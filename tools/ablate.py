@@ -2,8 +2,11 @@
 switched off (rn_set_debug_flags) interleaved in one process (rule 24 of
 cdna_hip_programming.md §5.4).  bit0: no grid atomics, bit1: no dW, bit2: no
 grid scatter at all, bit5 (32): rows staged but no walk (merged kernel).
-Token prefixes: none = merged backward, "s" = per-model backward, "i" =
-merged backward with integer accumulation, "f" = field_fwd."""
+Token prefixes: none = merged backward (fixed-point hashed levels: the
+_field call includes rn_grid_fx_fold and the redo launch), "x" = merged
+backward with fp32 grid atomics, "s" = per-model backward, "i" = merged
+backward with integer accumulation, "f" = field_fwd.
+Workload from ABL_K / ABL_SCALE / ABL_RAYS (default C3)."""
 import json
 import os
 import sys
@@ -51,9 +54,10 @@ def main():
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(int(f.lstrip("fsi")))
+            L.set_debug_flags(int(f.lstrip("fsix")))
             r.merged_bwd = not f.startswith("s")
             r.int_grad = f.startswith("i")
+            r.grid_fx = not f.startswith("x")      # "x": fp32 grid atomics
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             if f.startswith("f"):
