@@ -323,10 +323,23 @@ def main():
                 res_t = ml_render(model, gate, ot, dt_, dt_, test_time=True, exp_step_factor=esf)
             torch.cuda.synchronize()
             t_el = (time.perf_counter() - t0) / reps
+            # the reference's host-driven compaction loop on the same kernels
+            # (fused=False), once, for comparison
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            res_l = ml_render(model, gate, ot, dt_, dt_, test_time=True, exp_step_factor=esf,
+                              fused=False)
+            torch.cuda.synchronize()
+            t_loop = time.perf_counter() - t0
         test_time = {"rays": nt, "ms_per_image": round(t_el * 1e3, 3),
                      "Mrays_per_s": round(nt / t_el / 1e6, 3),
+                     "Msamples_per_s": round(float(res_t["total_samples"]) / t_el / 1e6, 1)
+                     if "total_samples" in res_t else None,
                      "opacity_mean": round(float(res_t["opacity"].mean()), 4),
-                     "path": "rendering.ml_render(test_time=True): host compaction loop"}
+                     "loop_ms_per_image": round(t_loop * 1e3, 3),
+                     "loop_vs_fused_rgb_linf": float((res_t["rgb"] - res_l["rgb"]).abs().max()),
+                     "path": "rendering.ml_render(test_time=True): rn_render_test (wave per ray); "
+                             "loop = the host compaction loop (fused=False)"}
     n_samples = samples_acc.clone()
     t_max = torch.tensor(elapsed, device=dev, dtype=torch.float64)
     if world > 1:

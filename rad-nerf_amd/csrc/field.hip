@@ -935,8 +935,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
     if (GM >= 2) {
-        fxA = __builtin_amdgcn_readfirstlane(F.scale[wid]);
-        fxB = __builtin_amdgcn_readfirstlane(F.scale[RN_L - 1 - wid]);
+        fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
+        fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
     }
     const bool do_sc = !(dbg & 4);
     float* sG = reinterpret_cast<float*>(sImg);

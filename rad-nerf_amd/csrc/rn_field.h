@@ -363,13 +363,29 @@ enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2,
 // forward of one 32-sample tile for the lanes' samples `s` (valid lanes only
 // load); fc: this lane's encoding-cache slot (CACHE_WRITE writes it on every
 // lane, CACHE_READ reads it on valid lanes)
+template <int CACHE>
+__device__ __forceinline__ void tile_forward_pos(const FieldArgs& a, const LvTab& T, const rn_half* W,
+                                                 float x, float y, float z, float dx, float dy,
+                                                 float dz, bool valid, half8* fc, FwdState& st,
+                                                 float& ux, float& uy, float& uz);
+
 template <int MODE, int CACHE>
 __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& T, const rn_half* W,
                                                int64_t s, bool valid, half8* fc, FwdState& st,
                                                float& ux, float& uy, float& uz) {
-    const int h = rn_lane() >> 5;
     float x = 0.f, y = 0.f, z = 0.f, dx = 1.f, dy = 0.f, dz = 0.f;
     if (valid) load_sample<MODE>(a, s, x, y, z, dx, dy, dz);
+    tile_forward_pos<CACHE>(a, T, W, x, y, z, dx, dy, dz, valid, fc, st, ux, uy, uz);
+}
+
+// the same for positions / directions already in registers (invalid lanes:
+// any finite values; their gathers are skipped)
+template <int CACHE>
+__device__ __forceinline__ void tile_forward_pos(const FieldArgs& a, const LvTab& T, const rn_half* W,
+                                                 float x, float y, float z, float dx, float dy,
+                                                 float dz, bool valid, half8* fc, FwdState& st,
+                                                 float& ux, float& uy, float& uz) {
+    const int h = rn_lane() >> 5;
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);

@@ -104,7 +104,7 @@ class _FieldFn(torch.autograd.Function):
     """MNGP.forward(x, d, ind) on rn_field_fwd / rn_field_bwd."""
 
     @staticmethod
-    def forward(ctx, xyzs, dirs, grid_params, mlp_params, model, ind):
+    def forward(ctx, xyzs, dirs, grid_params, mlp_params, model, ind, want_cache=True):
         xyzs = xyzs.float().contiguous()
         dirs = dirs.float().contiguous()
         n = xyzs.shape[0]
@@ -113,10 +113,11 @@ class _FieldFn(torch.autograd.Function):
         rgb = torch.empty(n, 3, device=dev)
         # encoding cache for the backward (64 B/sample): only when a gradient
         # will be asked for.  needs_input_grad reflects the parameters'
-        # requires_grad even under no_grad, so the grad mode is checked too
-        # (density-grid updates run under no_grad and skip the cache)
+        # requires_grad even under no_grad, and inside Function.forward grad
+        # mode is always off, so the caller's grad mode comes in as want_cache
+        # (no_grad renders and density-grid updates skip the cache)
         feat = None
-        if n > 0 and torch.is_grad_enabled() and any(ctx.needs_input_grad[:4]):
+        if n > 0 and want_cache and any(ctx.needs_input_grad[:4]):
             feat = torch.empty((n + 31) // 32 * 32, 32, device=dev, dtype=torch.float16)
         if n > 0:
             model._launch_field(True, xyzs, dirs, ind, sigma=sigma, rgb=rgb, feat=feat)
@@ -151,7 +152,7 @@ class _FieldFn(torch.autograd.Function):
                 dg = dd if dd is not None else torch.empty_like(dirs)
                 model._launch_dinput(xyzs, dirs, ind, ds, dr, xg, dg, feat=ctx.feat)
         ctx.feat = None
-        return dx, dd, grid_grad, dw, None, None
+        return dx, dd, grid_grad, dw, None, None, None
 
 
 class _DensityFn(torch.autograd.Function):
@@ -327,7 +328,8 @@ class MNGP(nn.Module):
 
     def forward(self, x, d, ind, **kwargs):
         """networks.py:311-328 -> sigmas (N), rgbs (N,3)"""
-        return _FieldFn.apply(x, d, self.xyz_encoder.params, self.mlp_params, self, ind)
+        return _FieldFn.apply(x, d, self.xyz_encoder.params, self.mlp_params, self, ind,
+                              torch.is_grad_enabled())
 
     @torch.no_grad()
     def get_all_cells(self):

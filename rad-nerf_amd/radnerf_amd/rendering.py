@@ -11,12 +11,18 @@ gradients within 1e-3) with fewer launches and no host synchronisation, 988 vs
 structure (RayAABBIntersector -> RayMarcher -> model(x, d, i) ->
 VolumeRenderer per sub-NeRF, then background and the gate-weighted combine).
 
-Test-time rendering follows the host-driven compaction loop of
-ml_rendering.py:81-155 / rendering.py:113-189.
+Test-time rendering (test_time=True) runs rn_render_test by default: one
+wave per ray marches, evaluates and composites its samples 32 at a time until
+the transmittance threshold, all sub-NeRFs in one launch, no host loop
+(render.hip).  `fused=False` keeps the host-driven compaction loop of
+ml_rendering.py:81-155 / rendering.py:113-189 (vren.raymarching_test + field +
+vren.composite_test_fw per round); both give the same per-ray results up to
+float rounding (tests/test_gpu_render.py).
 """
 import torch
 
 from . import vren
+from ._lib import lib
 from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
 
 MAX_SAMPLES = 1024
@@ -99,11 +105,50 @@ def _test_rays(model, rays_o, rays_d, hits_t, bitfield, call_model, kw):
             "total_samples": total, "deltas": deltas}
 
 
+@torch.no_grad()
+def _test_fused(model, rays_o, rays_d, hits_t, kw):
+    """Test-time renders of all model.size sub-NeRFs in one rn_render_test
+    launch; a list of per-sub-NeRF results with _test_rays' keys ('deltas' is
+    None: there are no per-round sample buffers)."""
+    K, B, dev = model.size, rays_o.shape[0], rays_o.device
+    esf = kw.get("exp_step_factor", 0.0)
+    bf = [getattr(model, f"density_bitfield_{i}") for i in range(K)]
+    nb = bf[0].numel()
+    bits = torch.stack([b.view(-1) for b in bf]).contiguous()
+    opacity = torch.empty(K, B, device=dev)
+    depth = torch.empty(K, B, device=dev)
+    rgb = torch.empty(K, B, 3, device=dev)
+    n_smp = torch.empty(K, B, device=dev, dtype=torch.int32)
+    queue = torch.empty(K, device=dev, dtype=torch.int32)
+    hits = hits_t[:, 0].contiguous()
+    enc = model.xyz_encoder
+    lo, lh, lr, ls = enc.level_ptrs()
+    # 4 waves per block, ~2 blocks per CU and sub-NeRF in flight; rays are
+    # handed out by ticket, so the grid only needs to fill the chip
+    blocks = max(1, min((B + 3) // 4, 512 // K))
+    if B > 0:
+        lib().render_test(rays_o.data_ptr(), rays_d.data_ptr(), hits.data_ptr(), B, K,
+                          bits.data_ptr(), nb, model.cascades, float(model.scale), float(esf),
+                          model.grid_size, int(kw.get("max_samples", MAX_SAMPLES)),
+                          enc.params_f16().data_ptr(), lo, lh, lr, ls, model._h_min.ctypes.data,
+                          model._h_ext.ctypes.data, model.packed_frags().data_ptr(),
+                          float(kw.get("T_threshold", 1e-4)), queue.data_ptr(),
+                          opacity.data_ptr(), depth.data_ptr(), rgb.data_ptr(), n_smp.data_ptr(),
+                          blocks, torch.cuda.current_stream(dev).cuda_stream)
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
+    return [{"opacity": opacity[i], "depth": depth[i],
+             "rgb": rgb[i] + bg * (1 - opacity[i])[:, None],
+             "total_samples": n_smp[i].sum(), "deltas": None} for i in range(K)]
+
+
 def render(model, rays_o, rays_d, **kwargs):
     """rendering.py:12-46 for a single NGP model."""
+    fused = kwargs.pop("fused", True)
     with torch.autocast("cuda"):
         rays_o, rays_d = rays_o.contiguous(), rays_d.contiguous()
         hits_t = _near_far(model, rays_o, rays_d)
+        if kwargs.get("test_time", False) and fused:
+            return _to_host(_test_fused(model, rays_o, rays_d, hits_t, kwargs)[0], kwargs)
         fn = _test_rays if kwargs.get("test_time", False) else _train_rays
         call = lambda x, d: model(x, d)
         res = fn(model, rays_o, rays_d, hits_t, model.density_bitfield, call, kwargs)
@@ -121,9 +166,7 @@ def _to_host(res, kw):
 def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):
     """ml_rendering.py:11-78: gate, K sub-NeRF renders, gate-weighted combine.
     fused (default: training renders) routes to radnerf_amd.fused."""
-    fused = kwargs.pop("fused", None)
-    if fused is None:
-        fused = not kwargs.get("test_time", False)
+    fused = kwargs.pop("fused", True)
     if fused and not kwargs.get("test_time", False):
         from .fused import ml_render_fused
         return ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup, **kwargs)
@@ -138,14 +181,24 @@ def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs)
         singles = []
         noise = kwargs.pop("noise", None)
         fn = _test_rays if kwargs.get("test_time", False) else _train_rays
+        test_fused = None
+        if kwargs.get("test_time", False) and fused:
+            # every sub-NeRF's test-time render in one launch (the same AABB
+            # interval for all of them, as the per-model _near_far below)
+            test_fused = _test_fused(model, rays_o, rays_d, _near_far(model, rays_o, rays_d),
+                                     kwargs)
         for i in range(K):
-            hits_t = _near_far(model, rays_o, rays_d)
-            kw = dict(kwargs)
-            if noise is not None:
-                kw["noise"] = noise[i]
-            call = lambda x, d, i=i: model(x, d, i)
-            r = fn(model, rays_o, rays_d, hits_t, getattr(model, f"density_bitfield_{i}"), call, kw)
-            r = _to_host(r, kwargs)
+            if test_fused is not None:
+                r = _to_host(test_fused[i], kwargs)
+            else:
+                hits_t = _near_far(model, rays_o, rays_d)
+                kw = dict(kwargs)
+                if noise is not None:
+                    kw["noise"] = noise[i]
+                call = lambda x, d, i=i: model(x, d, i)
+                r = fn(model, rays_o, rays_d, hits_t, getattr(model, f"density_bitfield_{i}"),
+                       call, kw)
+                r = _to_host(r, kwargs)
             singles.append(r["rgb"])
             rgb_acc = rgb_acc + r["rgb"] * gate[:, i][:, None]
             depth_all[:, i] = r["depth"]

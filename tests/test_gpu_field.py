@@ -85,6 +85,11 @@ def test_field_backward(cuda, zero_span):
     ind = 1
     m.zero_grad()
     sig, rgb = m(torch.from_numpy(x).to(cuda), torch.from_numpy(d).to(cuda), ind)
+    # the forward kept its encoding cache for this backward (grad mode on)
+    assert sig.grad_fn.feat is not None
+    with torch.no_grad():
+        s2, _ = m(torch.from_numpy(x).to(cuda), torch.from_numpy(d).to(cuda), ind)
+    assert s2.grad_fn is None and torch.equal(s2, sig)
     torch.autograd.backward([sig, rgb], [torch.from_numpy(ds).to(cuda), torch.from_numpy(dr).to(cuda)])
     osig, orgb, gp, mp = _oracle_field(m, x, d, ind, scale)
     torch.autograd.backward([osig, orgb], [torch.from_numpy(ds), torch.from_numpy(dr)])

@@ -8,6 +8,10 @@
 set -u
 mkdir -p gpurun_out
 TAG=${1:-r}
+# keep gpurun_out under the 64 MiB copy-back limit, whatever step ends the
+# script: the per-dispatch traces and counter rows are reduced on the box
+# (kernel stats, traffic_*.json)
+trap "find gpurun_out -name '*kernel_trace.csv' -delete; find gpurun_out -name '*counter_collection.csv' -delete" EXIT
 export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/tests_$TAG.log
