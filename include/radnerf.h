@@ -260,8 +260,8 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
  * 91-94 computes the same one per sub-NeRF); density_bitfields
  * [n_models][bitfield_bytes]; frags [n_models][46 * 512] f16.  Outputs per
  * (sub-NeRF, ray), without background: opacity / depth [n_models][n_rays],
- * rgb [n_models][n_rays][3], n_samples (marched) [n_models][n_rays].  queue:
- * n_models int32 scratch (ray tickets).  Replaces the host loop's
+ * rgb [n_models][n_rays][3], n_samples (marched) [n_models][n_rays].
+ * Replaces the host loop's
  * vren.raymarching_test + field + vren.composite_test_fw rounds.          */
 int rn_render_test(const float* rays_o, const float* rays_d, const float* hits_t, int64_t n_rays,
                    int32_t n_models, const uint8_t* density_bitfields, int64_t bitfield_bytes,
@@ -269,8 +269,8 @@ int rn_render_test(const float* rays_o, const float* rays_d, const float* hits_t
                    int32_t max_samples, const void* grid_f16, const uint32_t* level_offset,
                    const uint32_t* level_hsize, const uint32_t* level_res,
                    const float* level_scale, const float* xyz_min, const float* extent,
-                   const void* frags, float T_threshold, int32_t* queue, float* opacity,
-                   float* depth, float* rgb, int32_t* n_samples, int32_t blocks, void* stream);
+                   const void* frags, float T_threshold, float* opacity, float* depth,
+                   float* rgb, int32_t* n_samples, int32_t blocks, void* stream);
 
 /* Exact integer accumulation of the merged backward's grid gradient
  * (optional; igrad_lo == NULL keeps fp32 atomics into grid_grad).  With

@@ -46,11 +46,9 @@ struct RenderArgs {
     const uint8_t* bitfields;     // [K][bitfield_bytes]
     int64_t bitfield_bytes;
     MarchCfg mc;
-    int32_t* queue;               // [K] ray tickets (zeroed by the launcher)
     float* opacity; float* depth; float* rgb;   // [K][B], [K][B], [K][B][3]
     int32_t* n_samples;           // [K][B] samples marched
     int n_rays; int max_samples; float thr;
-    int dbg;                      // RN_RT_DBG bisection flags (dev only): 1 no march, 2 no field, 4 no composite
 };
 
 __device__ __forceinline__ float rd_lane(float v, int l) {
@@ -84,7 +82,7 @@ k_render_test(FieldArgs a, RenderArgs g) {
         for (;;) {
             if (++tiles > g.max_samples) { n_tot = -1; break; }    // cannot happen: n >= 1 per tile
             const int cap = min(32, g.max_samples - n_tot);
-            const int n = __builtin_amdgcn_readfirstlane((g.dbg & 1) ? 0 : march_ray_wave<true, TileSink, true>(
+            const int n = __builtin_amdgcn_readfirstlane(march_ray_wave<true, TileSink, true>(
                 ox, oy, oz, dx, dy, dz, t, t2, cap, 0, bits, g.mc, sink));
             n_tot += n;
             if (n == 0) break;
@@ -100,16 +98,15 @@ k_render_test(FieldArgs a, RenderArgs g) {
             const float x = fmaf(tc, dx, ox), y = fmaf(tc, dy, oy), z = fmaf(tc, dz, oz);
             FwdState st;
             float ux, uy, uz;
-            if (g.dbg & 2) { st.g0 = 0.f; st.out = rn_zero16(); }
-            else tile_forward_pos<CACHE_NONE>(a, sT, sW, x, y, z, dx, dy, dz, valid, nullptr, st,
-                                              ux, uy, uz);
+            tile_forward_pos<CACHE_NONE>(a, sT, sW, x, y, z, dx, dy, dz, valid, nullptr, st,
+                                         ux, uy, uz);
             // lanes 0..31 (h == 0) hold sample c's outputs, as rn_field_fwd writes them
             const float sig = expf(st.g0);
             const float r0 = sigmoidf(st.out[0]), r1 = sigmoidf(st.out[1]), r2 = sigmoidf(st.out[2]);
             // volumerendering.cu:206-286 in its order and arithmetic
             float T = 1.0f - co;
             bool stop = false;
-            for (int s = 0; s < ((g.dbg & 4) ? 0 : n); ++s) {
+            for (int s = 0; s < n; ++s) {
                 const float ts_ = rd_lane(tc, s), dl = rd_lane(dtc, s);
                 const float al = 1.0f - rn_exp_det(-rd_lane(sig, s) * dl);
                 const float w = al * T;
@@ -144,14 +141,14 @@ int rn_render_test(const float* rays_o, const float* rays_d, const float* hits_t
                    int32_t max_samples, const void* grid_f16, const uint32_t* level_offset,
                    const uint32_t* level_hsize, const uint32_t* level_res,
                    const float* level_scale, const float* xyz_min, const float* extent,
-                   const void* frags, float T_threshold, int32_t* queue, float* opacity,
+                   const void* frags, float T_threshold, float* opacity,
                    float* depth, float* rgb, int32_t* n_samples, int32_t blocks, void* stream) {
     RN_CHECK_ARG(n_rays >= 0 && n_rays < (1ll << 31) && n_models >= 1 && cascades >= 1 &&
                  grid_size >= 1 && max_samples >= 1 && blocks >= 1 && bitfield_bytes >= 1,
                  "bad sizes");
     if (n_rays == 0) return 0;
     RN_CHECK_ARG(rays_o && rays_d && hits_t && density_bitfields && grid_f16 && level_offset &&
-                 level_hsize && level_res && level_scale && xyz_min && extent && frags && queue &&
+                 level_hsize && level_res && level_scale && xyz_min && extent && frags &&
                  opacity && depth && rgb && n_samples, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
@@ -162,15 +159,9 @@ int rn_render_test(const float* rays_o, const float* rays_d, const float* hits_t
     // raymarching.cu:370,399: the test march hands `cascades` to calc_dt as its scale
     g.mc.cascades = cascades; g.mc.grid_size = grid_size; g.mc.max_samples = max_samples;
     g.mc.scale = scale; g.mc.dt_scale = (float)cascades; g.mc.esf = exp_step_factor;
-    g.queue = queue; g.opacity = opacity; g.depth = depth; g.rgb = rgb; g.n_samples = n_samples;
+    g.opacity = opacity; g.depth = depth; g.rgb = rgb; g.n_samples = n_samples;
     g.n_rays = (int)n_rays; g.max_samples = max_samples; g.thr = T_threshold;
-    const char* dbg = getenv("RN_RT_DBG");
-    g.dbg = dbg ? atoi(dbg) : 0;
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(queue, 0, sizeof(int32_t) * n_models, st) != hipSuccess) {
-        rn_set_error("%s: ticket reset failed", __func__);
-        return 2;
-    }
     k_render_test<<<dim3(blocks, n_models), RT_WAVES * 64, 0, st>>>(a, g);
     RN_CHECK_LAUNCH();
     return 0;

@@ -55,7 +55,7 @@ SIGNATURES = {
                             P, I32, P],
     "rn_grid_fx_fold": [P, P, P, P, P, P, P, P, P, P],
     "rn_render_test": [P, P, P, I64, I32, P, I64, I32, F32, F32, I32, I32, P, P, P, P, P, P, P,
-                       P, F32, P, P, P, P, P, I32, P],
+                       P, F32, P, P, P, P, I32, P],
     "rn_seed_scale": [P, P, I32, P, P, P, P, P, P],
     "rn_igrad_to_f32": [I64, P, P, P, P, P],
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,

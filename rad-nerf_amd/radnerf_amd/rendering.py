@@ -119,12 +119,11 @@ def _test_fused(model, rays_o, rays_d, hits_t, kw):
     depth = torch.empty(K, B, device=dev)
     rgb = torch.empty(K, B, 3, device=dev)
     n_smp = torch.empty(K, B, device=dev, dtype=torch.int32)
-    queue = torch.empty(K, device=dev, dtype=torch.int32)
     hits = hits_t[:, 0].contiguous()
     enc = model.xyz_encoder
     lo, lh, lr, ls = enc.level_ptrs()
-    # 4 waves per block, ~2 blocks per CU and sub-NeRF in flight; rays are
-    # handed out by ticket, so the grid only needs to fill the chip
+    # 4 waves per block, ~2 blocks per CU and sub-NeRF in flight; rays go
+    # round-robin over the waves, so the grid only needs to fill the chip
     blocks = max(1, min((B + 3) // 4, 512 // K))
     if B > 0:
         lib().render_test(rays_o.data_ptr(), rays_d.data_ptr(), hits.data_ptr(), B, K,
@@ -132,8 +131,7 @@ def _test_fused(model, rays_o, rays_d, hits_t, kw):
                           model.grid_size, int(kw.get("max_samples", MAX_SAMPLES)),
                           enc.params_f16().data_ptr(), lo, lh, lr, ls, model._h_min.ctypes.data,
                           model._h_ext.ctypes.data, model.packed_frags().data_ptr(),
-                          float(kw.get("T_threshold", 1e-4)), queue.data_ptr(),
-                          opacity.data_ptr(), depth.data_ptr(), rgb.data_ptr(), n_smp.data_ptr(),
+                          float(kw.get("T_threshold", 1e-4)), opacity.data_ptr(), depth.data_ptr(), rgb.data_ptr(), n_smp.data_ptr(),
                           blocks, torch.cuda.current_stream(dev).cuda_stream)
     bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
     return [{"opacity": opacity[i], "depth": depth[i],

@@ -18,7 +18,7 @@ rc=$?; echo "pytest rc=$rc" >> gpurun_out/tests_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
-Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0"
+Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0 --test-time-rays 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py $Q --steps 10 --warmup 3 > gpurun_out/prof_$TAG.log 2>&1 || exit $?
 cp profiles/traffic.json gpurun_out/traffic.json
 pmc() {   # $1 = name, rest = bench args

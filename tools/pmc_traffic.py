@@ -99,7 +99,9 @@ def main():
                 allw = json.load(f)
         except (OSError, ValueError):
             allw = {}
-        allw.setdefault("workloads", {})[key] = out
+        # keep the entry's other fields (u32_request_share: the replay's split
+        # of the requests between fp32 and u32 adds)
+        allw.setdefault("workloads", {}).setdefault(key, {}).update(out)
         with open(merge, "w") as f:
             json.dump(allw, f, indent=1)
             f.write("\n")
