@@ -28,16 +28,35 @@ def main():
     m = MNGP(scale, size=2, seed=3).to(dev)
     thr = 0.01 * 1024 / 3 ** 0.5
     rdist.update_density_grid(m, thr, 0, warmup=True)
+    if len(sys.argv) > 2:       # occupied fraction of a trained scene: densities above thr
+        occ = float(sys.argv[2])
+        with torch.no_grad():
+            for i in range(m.size):
+                d = getattr(m, f"density_grid_{i}")
+                d.copy_(torch.where(torch.rand_like(d) < occ, 2 * thr, 0.5 * thr))
     g = rdist.step_generator(dev, 0, 1)
     M = 128 ** 3 // 4
     dg = m.density_grid_0
-    out = {"warmup": t(lambda: rdist.update_density_grid(m, thr, 0, warmup=True)),
-           "sampled": t(lambda: rdist.update_density_grid(m, thr, 1, warmup=False)),
+    saved = {n: b.clone() for n, b in m.named_buffers() if "density" in n}
+
+    def restore():
+        with torch.no_grad():
+            for n, b in m.named_buffers():
+                if n in saved:
+                    b.copy_(saved[n])
+
+    def sampled():
+        restore()
+        rdist.update_density_grid(m, thr, 1, warmup=False)
+
+    out = {"restore": t(restore),
+           "sampled": t(sampled),
            "randint": t(lambda: torch.randint(128, (M, 3), dtype=torch.int32, device=dev, generator=g)),
            "nonzero": t(lambda: torch.nonzero(dg[0] > thr)[:, 0]),
            "cells": t(lambda: m.sample_uniform_and_occupied_cells(M, thr, 0, g)),
            "density_1M": t(lambda: m.density(torch.rand(2 * M, 3, device=dev) - 0.5, 0)),
-           "occupied_frac": float((dg > thr).float().mean())}
+           "occupied_frac": float((dg > thr).float().mean()),
+           "warmup": t(lambda: rdist.update_density_grid(m, thr, 0, warmup=True))}
     print(out)
 
 
