@@ -25,7 +25,8 @@ def t(fn, n=5):
 def main():
     dev = torch.device("cuda")
     scale = float(sys.argv[1]) if len(sys.argv) > 1 else 0.5
-    m = MNGP(scale, size=2, seed=3).to(dev)
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    m = MNGP(scale, size=K, seed=3).to(dev)
     thr = 0.01 * 1024 / 3 ** 0.5
     rdist.update_density_grid(m, thr, 0, warmup=True)
     if len(sys.argv) > 2:       # occupied fraction of a trained scene: densities above thr
