@@ -345,6 +345,27 @@ int rn_field_dinput(const float* xyzs, const float* dirs, int64_t n_samples, con
                     const void* frags, const void* dinput_frags, const float* dL_dsigma,
                     const float* dL_drgb, const void* feat_cache, float* dL_dxyz,
                     float* dL_ddir, int32_t blocks_per_model, void* stream);
+/* Sampled occupancy-grid update on the device (MNGP.update_density_grid
+ * with warmup False, networks.py:345-409, train_ml.py:174-177), all n_models
+ * sub-NeRFs and cascades in one call, no host synchronisation.  grid_ptrs /
+ * bitfield_ptrs: device arrays of n_models pointers to the (cascades, 128^3)
+ * f32 density grids (updated in place) and their bitfields.  Per (sub-NeRF,
+ * cascade): 128^3/4 uniform cells and 128^3/4 cells drawn among those with
+ * density > threshold, jittered in the cell, drawn from a counter-based hash
+ * of `seed` (same seed -> same cells on every rank); sigma from the grid + geo
+ * MLP (frags: [n_models][46 * 512] f16); duplicates keep their max; then
+ * grid = grid < 0 ? grid : max(grid * decay, sampled), packbits at
+ * min(mean of the positive cells, threshold) (thr_out [n_models]).
+ * Scratch: tmp, occ (n_models * cascades * 128^3 f32 / i32), blk
+ * (n_models * cascades * 128^3 / 1024 + 1 i32), part (n_models * 1024 f32).   */
+int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, int32_t n_models,
+                              int32_t cascades, int32_t grid_size, float scale,
+                              float density_threshold, float decay, uint64_t seed,
+                              const void* grid_f16, const uint32_t* level_offset,
+                              const uint32_t* level_hsize, const uint32_t* level_res,
+                              const float* level_scale, const float* xyz_min, const float* extent,
+                              const void* frags, float* tmp, int32_t* occ, int32_t* blk,
+                              float* part, float* thr_out, void* stream);
 int rn_field_density(const float* xyzs, int64_t n_samples, const void* grid_f16,
                      const uint32_t* level_offset, const uint32_t* level_hsize,
                      const uint32_t* level_res, const float* level_scale, const float* xyz_min,

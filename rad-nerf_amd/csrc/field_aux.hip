@@ -308,6 +308,240 @@ k_field_density(FieldArgs a, float* __restrict__ feat_out) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Sampled occupancy-grid update on the device (networks.py:345-409 with
+// warmup False, all K sub-NeRFs and C cascades per launch, no host sync).
+// Cells: per (sub-NeRF k, cascade c) M uniform cells and M cells drawn
+// uniformly among those with density > threshold, jittered in the cell; the
+// draws come from a counter-based hash of (seed, k, c, i, stream) instead of
+// torch's generator (same distribution; identical on every rank for the same
+// seed, which is what ray-batch data parallelism needs).
+// ---------------------------------------------------------------------------
+#define DU_BLK 1024        // elements per compaction block (G^3 is a multiple)
+
+__device__ __forceinline__ uint64_t du_mix(uint64_t z) {      // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ uint32_t du_hash(uint64_t seed, uint32_t seg, uint32_t i, uint32_t st) {
+    return (uint32_t)(du_mix(seed * 0x9e3779b97f4a7c15ull + (((uint64_t)seg << 32) | i) +
+                             (uint64_t)st * 0xd1b54a32d192ed03ull) >> 32);
+}
+__device__ __forceinline__ float du_unit(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
+
+struct DensityUpd {
+    const float* const* grids;      // [K] -> (C, G3) density grids
+    uint8_t* const* bitfields;      // [K] -> C G3 / 8 bytes
+    float* tmp;                     // (K, C, G3) sampled sigma, zero on entry
+    int32_t* occ;                   // (K C G3) occupied cells, segment-ordered
+    int32_t* blk;                   // (K C G3 / DU_BLK + 1) per-block counts -> offsets
+    float* part;                    // (K, DU_PART, 2) partial sums / counts of positives
+    float* thr_out;                 // [K] packbits threshold min(mean, thr)
+    uint64_t seed;
+    int K, C, G, M;
+    float thr, decay, scale;
+};
+#define DU_PART 512
+
+// 1. per-block count of occupied cells (dg > thr) over all (k, c)
+__global__ void __launch_bounds__(256)
+k_du_count(DensityUpd u) {
+    const int64_t G3 = (int64_t)u.G * u.G * u.G, seg_blocks = G3 / DU_BLK;
+    const int64_t b = blockIdx.x;
+    const int64_t seg = b / seg_blocks, k = seg / u.C, c = seg % u.C;
+    const float* g = u.grids[k] + c * G3 + (b % seg_blocks) * DU_BLK;
+    int n = 0;
+    for (int j = threadIdx.x; j < DU_BLK; j += blockDim.x) n += g[j] > u.thr;
+    __shared__ int sN;
+    if (threadIdx.x == 0) sN = 0;
+    __syncthreads();
+    n = (int)rn_wave_sum((float)n);
+    if (rn_lane() == 0) atomicAdd(&sN, n);
+    __syncthreads();
+    if (threadIdx.x == 0) u.blk[b] = sN;
+}
+
+// 2. exclusive scan of the block counts (one block, fixed order)
+__global__ void __launch_bounds__(1024)
+k_du_scan(DensityUpd u, int nb) {
+    __shared__ int sPart[1024];
+    const int t = threadIdx.x, per = (nb + 1023) / 1024;
+    int acc = 0;
+    for (int j = 0; j < per; ++j) { const int q = t * per + j; if (q < nb) acc += u.blk[q]; }
+    sPart[t] = acc;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {           // Hillis-Steele, inclusive
+        const int v = t >= off ? sPart[t - off] : 0;
+        __syncthreads();
+        sPart[t] += v;
+        __syncthreads();
+    }
+    int run = t ? sPart[t - 1] : 0;
+    for (int j = 0; j < per; ++j) {
+        const int q = t * per + j;
+        if (q < nb) { const int v = u.blk[q]; u.blk[q] = run; run += v; }
+    }
+    if (t == 1023) u.blk[nb] = sPart[1023];
+}
+
+// 3. ordered write of the occupied cells: segment-relative cell index j
+__global__ void __launch_bounds__(256)
+k_du_write(DensityUpd u) {
+    const int64_t G3 = (int64_t)u.G * u.G * u.G, seg_blocks = G3 / DU_BLK;
+    const int64_t b = blockIdx.x;
+    const int64_t seg = b / seg_blocks, k = seg / u.C, c = seg % u.C;
+    const int64_t j0 = (b % seg_blocks) * DU_BLK;
+    const float* g = u.grids[k] + c * G3 + j0;
+    __shared__ int sWave[4];
+    int base = u.blk[b];
+    for (int j = 0; j < DU_BLK; j += blockDim.x) {
+        const bool o = g[j + threadIdx.x] > u.thr;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(o);
+        const int w = threadIdx.x / RN_WAVE;
+        if (rn_lane() == 0) sWave[w] = __builtin_popcountll(m);
+        __syncthreads();
+        int before = 0;
+        for (int q = 0; q < w; ++q) before += sWave[q];
+        const int tot = sWave[0] + sWave[1] + sWave[2] + sWave[3];
+        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        if (o) u.occ[base + before + r] = (int32_t)(j0 + j + threadIdx.x);
+        base += tot;
+        __syncthreads();
+    }
+}
+
+// 4. draw, jitter, sigma (grid + geo MLP, as k_field_density) and scatter-max
+// of sample i of segment (k, c): i < M uniform, else occupied (skipped when
+// the segment has no occupied cell).  blockIdx.y = k.
+__global__ void __launch_bounds__(256)
+k_du_sample(FieldArgs a, DensityUpd u) {
+    __shared__ __attribute__((aligned(16))) rn_half sW[8 * RN_FRAG_HALFS];
+    __shared__ LvTab sT;
+    const int k = blockIdx.y;
+    rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS, 8 * RN_FRAG_BYTES);
+    lv_stage(sT, a.gm);
+    __syncthreads();
+    const int64_t G3 = (int64_t)u.G * u.G * u.G, seg_blocks = G3 / DU_BLK;
+    const int64_t per_seg = 2 * (int64_t)u.M, n = per_seg * u.C;
+    const int64_t n_tiles = (n + 31) / 32;
+    const int waves = blockDim.x / RN_WAVE;
+    const int lane = rn_lane(), cl = lane & 31, h = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = rn_rsrc(a.grid, a.grid_bytes);
+    for (int64_t tile = (int64_t)blockIdx.x * waves + threadIdx.x / RN_WAVE; tile < n_tiles;
+         tile += (int64_t)gridDim.x * waves) {
+        rn_lds_order();
+        const int64_t q = tile * 32 + cl;
+        bool valid = q < n;
+        const int c = valid ? (int)(q / per_seg) : 0;
+        const uint32_t i = valid ? (uint32_t)(q % per_seg) : 0u;
+        const int seg = k * u.C + c;
+        uint32_t cell = 0;
+        if (valid) {
+            if (i < (uint32_t)u.M) {
+                cell = du_hash(u.seed, seg, i, 0) & (uint32_t)(G3 - 1);     // G3 = 2^21
+            } else {
+                const int32_t o0 = u.blk[(int64_t)seg * seg_blocks];
+                const int32_t no = u.blk[(int64_t)(seg + 1) * seg_blocks] - o0;
+                if (no > 0) {
+                    const uint32_t r = (uint32_t)(((uint64_t)du_hash(u.seed, seg, i, 1) * (uint32_t)no) >> 32);
+                    cell = (uint32_t)u.occ[o0 + r];
+                } else {
+                    valid = false;
+                }
+            }
+        }
+        // networks.py:386-391: cell centre of cascade c, jittered by +-half a cell
+        const float sc = fminf(scalbnf(1.0f, c - 1), u.scale);
+        const float hgs = sc / u.G;
+        const float gm1 = (float)(u.G - 1);
+        const float cx = (float)rn_morton3d_invert(cell), cy = (float)rn_morton3d_invert(cell >> 1),
+                    cz = (float)rn_morton3d_invert(cell >> 2);
+        const float jx = du_unit(du_hash(u.seed, seg, i, 2)), jy = du_unit(du_hash(u.seed, seg, i, 3)),
+                    jz = du_unit(du_hash(u.seed, seg, i, 4));
+        const float x = ((cx / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jx * 2.0f - 1.0f) * hgs;
+        const float y = ((cy / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jy * 2.0f - 1.0f) * hgs;
+        const float z = ((cz / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jz * 2.0f - 1.0f) * hgs;
+        const float ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
+        const float uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
+        const float uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
+        half8 e0, e1;
+        encode_lane(a, sT, rs, h, ux, uy, uz, valid, e0, e1);
+        f32x16 a0 = rn_zero16(), a1 = rn_zero16();
+        a0 = rn_mfma(rn_frag(sW, 0), e0, a0); a0 = rn_mfma(rn_frag(sW, 1), e1, a0);
+        a1 = rn_mfma(rn_frag(sW, 2), e0, a1); a1 = rn_mfma(rn_frag(sW, 3), e1, a1);
+        half8 h1[4];
+        rn_acc_to_frags<true>(a0, h1[0], h1[1]);
+        rn_acc_to_frags<true>(a1, h1[2], h1[3]);
+        f32x16 gg = rn_zero16();
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq) gg = rn_mfma(rn_frag(sW, 4 + qq), h1[qq], gg);
+        if (valid && h == 0) {
+            // duplicate cells keep their max (deterministic, as rn_scatter_max)
+            const float sig = expf(gg[8]);
+            atomicMax(reinterpret_cast<int*>(u.tmp) + (int64_t)seg * G3 + cell,
+                      __float_as_int(fmaxf(sig, 0.0f)));
+        }
+    }
+}
+
+// 5. grid = dg < 0 ? dg : max(dg * decay, tmp) in place; per-block partial sum
+// and count of the positive cells (fixed slots: the mean is deterministic)
+__global__ void __launch_bounds__(256)
+k_du_decay(DensityUpd u) {
+    const int k = blockIdx.y;
+    const int64_t n = (int64_t)u.C * u.G * u.G * u.G;
+    float* g = const_cast<float*>(u.grids[k]);
+    const float* t = u.tmp + (int64_t)k * n;
+    float s = 0.f, cnt = 0.f;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const float d = g[e];
+        const float v = d < 0.f ? d : fmaxf(d * u.decay, t[e]);
+        g[e] = v;
+        if (v > 0.f) { s += v; cnt += 1.f; }
+    }
+    __shared__ float sS[4], sC[4];
+    s = rn_wave_sum(s); cnt = rn_wave_sum(cnt);
+    const int w = threadIdx.x / RN_WAVE;
+    if (rn_lane() == 0) { sS[w] = s; sC[w] = cnt; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        u.part[((int64_t)k * DU_PART + blockIdx.x) * 2] = (sS[0] + sS[1]) + (sS[2] + sS[3]);
+        u.part[((int64_t)k * DU_PART + blockIdx.x) * 2 + 1] = (sC[0] + sC[1]) + (sC[2] + sC[3]);
+    }
+}
+
+// 6. mean of the positive densities -> threshold min(mean, thr), per model
+__global__ void __launch_bounds__(64)
+k_du_mean(DensityUpd u) {
+    const int k = blockIdx.x;
+    double s = 0.0, c = 0.0;
+    if (threadIdx.x == 0) {
+        for (int b = 0; b < DU_PART; ++b) {
+            s += u.part[((int64_t)k * DU_PART + b) * 2];
+            c += u.part[((int64_t)k * DU_PART + b) * 2 + 1];
+        }
+        const float mean = c > 0.0 ? (float)(s / c) : 0.f;
+        u.thr_out[k] = fminf(mean, u.thr);
+    }
+}
+
+// 7. packbits (raymarching.cu:141-161) at the device threshold
+__global__ void __launch_bounds__(256)
+k_du_pack(DensityUpd u) {
+    const int k = blockIdx.y;
+    const int64_t n_bytes = (int64_t)u.C * u.G * u.G * u.G / 8;
+    const int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= n_bytes) return;
+    const float th = u.thr_out[k];
+    const float* g = u.grids[k] + 8 * b;
+    uint32_t bits = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bits |= (g[j] > th ? 1u : 0u) << j;
+    u.bitfields[k][b] = (uint8_t)bits;
+}
+
 inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 }  // namespace
@@ -348,6 +582,48 @@ int rn_field_dinput(const float* xyzs, const float* dirs, int64_t n_samples, con
         if (feat_cache) k_field_dinput<1, CACHE_READ><<<grid, DIN_WAVES * 64, 0, st>>>(a, df, dL_dxyz, dL_ddir);
         else k_field_dinput<1, CACHE_NONE><<<grid, DIN_WAVES * 64, 0, st>>>(a, df, dL_dxyz, dL_ddir);
     }
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, int32_t n_models,
+                              int32_t cascades, int32_t grid_size, float scale,
+                              float density_threshold, float decay, uint64_t seed,
+                              const void* grid_f16, const uint32_t* level_offset,
+                              const uint32_t* level_hsize, const uint32_t* level_res,
+                              const float* level_scale, const float* xyz_min, const float* extent,
+                              const void* frags, float* tmp, int32_t* occ, int32_t* blk,
+                              float* part, float* thr_out, void* stream) {
+    RN_CHECK_ARG(n_models >= 1 && cascades >= 1 && grid_size == 128, "bad sizes (grid_size 128)");
+    RN_CHECK_ARG(grid_ptrs && bitfield_ptrs && grid_f16 && level_offset && level_hsize &&
+                 level_res && level_scale && xyz_min && extent && frags && tmp && occ && blk &&
+                 part && thr_out, "null pointer");
+    FieldArgs a{};
+    fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
+    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
+    DensityUpd u{};
+    u.grids = (const float* const*)grid_ptrs; u.bitfields = (uint8_t* const*)bitfield_ptrs;
+    u.tmp = tmp; u.occ = occ; u.blk = blk; u.part = part; u.thr_out = thr_out;
+    u.seed = seed; u.K = n_models; u.C = cascades; u.G = grid_size;
+    const int64_t G3 = (int64_t)grid_size * grid_size * grid_size;
+    u.M = (int)(G3 / 4);                                  // networks.py:378: grid_size**3 // 4
+    u.thr = density_threshold; u.decay = decay; u.scale = scale;
+    hipStream_t st = (hipStream_t)stream;
+    const int64_t n_all = (int64_t)n_models * cascades * G3;
+    const int nb = (int)(n_all / DU_BLK);
+    if (hipMemsetAsync(tmp, 0, sizeof(float) * n_all, st) != hipSuccess) {
+        rn_set_error("%s: memset failed", __func__);
+        return 2;
+    }
+    k_du_count<<<nb, 256, 0, st>>>(u);
+    k_du_scan<<<1, 1024, 0, st>>>(u, nb);
+    k_du_write<<<nb, 256, 0, st>>>(u);
+    const int64_t tiles = (2 * (int64_t)u.M * cascades + 31) / 32;
+    const int sb = (int)(tiles / 4 + 1 < 2048 ? tiles / 4 + 1 : 2048);
+    k_du_sample<<<dim3(sb, n_models), 256, 0, st>>>(a, u);
+    k_du_decay<<<dim3(DU_PART, n_models), 256, 0, st>>>(u);
+    k_du_mean<<<n_models, 64, 0, st>>>(u);
+    k_du_pack<<<dim3(nblk(cascades * G3 / 8, 256), n_models), 256, 0, st>>>(u);
     RN_CHECK_LAUNCH();
     return 0;
 }

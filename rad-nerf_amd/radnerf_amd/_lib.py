@@ -17,6 +17,7 @@ I32 = ctypes.c_int32
 I64 = ctypes.c_int64
 F32 = ctypes.c_float
 F64 = ctypes.c_double
+U64 = ctypes.c_uint64
 
 # name -> argtypes (all return int status).  Keep in sync with include/radnerf.h
 SIGNATURES = {
@@ -27,6 +28,8 @@ SIGNATURES = {
     "rn_field_dinput": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                         P, I32, P],
     "rn_field_density": [P, I64, P, P, P, P, P, P, P, P, P, P, P],
+    "rn_density_update_sampled": [P, P, I32, I32, I32, F32, F32, F32, U64, P, P, P, P, P, P, P,
+                                  P, P, P, P, P, P, P],
     "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "rn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
     "rn_raymarching_train_count": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P],

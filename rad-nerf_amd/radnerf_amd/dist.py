@@ -99,7 +99,13 @@ def step_generator(device, seed, step):
 
 def update_density_grid(model, density_threshold, step, warmup=False, seed=0, decay=0.95):
     """train_ml.py:174-177 (model.update_density_grid every update_interval
-    steps) made rank-consistent: the cell draws and jitter come from
-    step_generator(seed, step), identical on every rank."""
-    g = step_generator(model.mlp_params.device, seed, step)
-    model.update_density_grid(density_threshold, warmup=warmup, decay=decay, generator=g)
+    steps) made rank-consistent: the warm-up's jitter comes from
+    step_generator(seed, step), the sampled update's cells and jitter from the
+    device-side hash of the same (seed, step) -- identical on every rank."""
+    if warmup:
+        g = step_generator(model.mlp_params.device, seed, step)
+        model.update_density_grid(density_threshold, warmup=True, decay=decay, generator=g)
+    else:
+        # device-side draws from a hash of (seed, step): the same on every rank
+        model.update_density_grid(density_threshold, warmup=False, decay=decay,
+                                  seed=(int(seed) * 1000003 + int(step)) & 0x7FFFFFFFFFFFFFFF)

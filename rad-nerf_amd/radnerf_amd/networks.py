@@ -360,8 +360,12 @@ class MNGP(nn.Module):
 
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False,
-                            generator=None):
-        """networks.py:375-409.  `generator` (a torch.Generator on the model's
+                            generator=None, seed=None):
+        """networks.py:375-409.  With `seed` (an int), the sampled update
+        (warmup False) runs on the device in one call for every sub-NeRF and
+        cascade (rn_density_update_sampled: cell draws from a counter-based
+        hash of the seed, no host synchronisation); radnerf_amd.dist and the
+        Trainer pass the step's seed.  `generator` (a torch.Generator on the model's
         device) replaces torch's default random stream for the cell draws and
         the jitter: with ray-batch data parallelism every rank passes one
         seeded identically (radnerf_amd.dist.update_density_grid), so the
@@ -369,6 +373,8 @@ class MNGP(nn.Module):
         deterministic kernels, keep bit-identical grids and bitfields with no
         collective.  sigma comes from the density-only kernel (rn_field_density:
         hash grid + geo MLP, networks.py:393-394)."""
+        if seed is not None and not warmup:
+            return self._update_sampled_device(density_threshold, decay, seed)
         for i in range(self.size):
             density_grid = getattr(self, f"density_grid_{i}")
             density_bitfield = getattr(self, f"density_bitfield_{i}")
@@ -398,6 +404,41 @@ class MNGP(nn.Module):
             vren.packbits(density_grid.contiguous(), min(mean_density, density_threshold),
                           density_bitfield)
             setattr(self, f"density_grid_{i}", density_grid)
+
+    @torch.no_grad()
+    def _update_sampled_device(self, density_threshold, decay, seed):
+        """The sampled update of every sub-NeRF in one rn_density_update_sampled
+        call; the density grids and bitfields are updated in place."""
+        K, C, G = self.size, self.cascades, self.grid_size
+        dev = self.mlp_params.device
+        n = K * C * G ** 3
+        du = getattr(self, "_du", None)
+        if du is None or du["tmp"].numel() != n or du["tmp"].device != dev:
+            du = {"tmp": torch.empty(n, device=dev),
+                  "occ": torch.empty(n, device=dev, dtype=torch.int32),
+                  "blk": torch.empty(n // 1024 + 1, device=dev, dtype=torch.int32),
+                  "part": torch.empty(K * 1024, device=dev),
+                  "thr": torch.empty(K, device=dev)}
+            self._du = du
+        grids = [getattr(self, f"density_grid_{i}") for i in range(K)]
+        bits = [getattr(self, f"density_bitfield_{i}") for i in range(K)]
+        for i, g in enumerate(grids):
+            if not (g.is_contiguous() and g.dtype == torch.float32 and g.numel() == C * G ** 3):
+                g = g.float().contiguous()
+                setattr(self, f"density_grid_{i}", g)
+                grids[i] = g
+        ptrs = torch.tensor([g.data_ptr() for g in grids] + [b.data_ptr() for b in bits],
+                            dtype=torch.int64).to(dev, non_blocking=True)
+        lo, lh, lr, ls = self.xyz_encoder.level_ptrs()
+        lib().density_update_sampled(
+            ptrs.data_ptr(), ptrs.data_ptr() + 8 * K, K, C, G, float(self.scale),
+            float(density_threshold), float(decay), int(seed) & 0xFFFFFFFFFFFFFFFF,
+            self.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
+            self._h_ext.ctypes.data, self.packed_frags().data_ptr(), du["tmp"].data_ptr(),
+            du["occ"].data_ptr(), du["blk"].data_ptr(), du["part"].data_ptr(),
+            du["thr"].data_ptr(), _stream(dev))
+        self._du_ptrs = ptrs          # keep the pointer array alive until the launch ran
+        return du
 
     @torch.no_grad()
     def register_bbox(self, bbox):

@@ -198,3 +198,59 @@ def test_image_gate(cuda, scale):
     assert np.abs(ref["gate"] - ml_oracle.ml_train_step(
         o, d, bits, noise, m.xyz_encoder.params.detach().cpu().view(-1, 2),
         m.mlp_params.detach().cpu(), g.params.detach().cpu(), scale)["gate"]).max() > 1e-3
+
+
+@pytest.mark.parametrize("scale,K", [(0.5, 2), (16.0, 3)])
+def test_density_update_sampled_device(cuda, scale, K):
+    """rn_density_update_sampled (networks.py:345-409, warmup False, all
+    sub-NeRFs and cascades in one call): per (sub-NeRF, cascade) M = G^3/4
+    uniform cells and M cells among the occupied ones.  Coverage of the draws
+    per segment (sigma > 0 everywhere, so a sampled cell has tmp > 0): free
+    cells 1 - e^-1/4, occupied cells 1 - e^-3/4; a segment without occupied
+    cells gets only the uniform draws.  Decay / max, negative cells untouched,
+    packbits at min(mean of the positive cells, thr); the same seed gives
+    identical grids and bitfields, another seed other cells."""
+    m = MNGP(scale, size=K, seed=3).to(cuda)
+    C, G3 = m.cascades, m.grid_size ** 3
+    thr = 0.01 * 1024 / 3 ** 0.5
+    gen = torch.Generator(device=cuda)
+    gen.manual_seed(1)
+    occ_mask = torch.rand(K, C, G3, generator=gen, device=cuda) < 0.5
+    occ_mask[0, 0] = False                       # one segment without occupied cells
+    old = torch.where(occ_mask, 2 * thr, 0.0)
+    old[:, :, :1000] = -1.0                      # cells the update must leave alone
+    outs, tmps = [], []
+    for seed in (77, 77, 78):
+        with torch.no_grad():
+            for i in range(K):
+                getattr(m, f"density_grid_{i}").copy_(old[i])
+        du = m.update_density_grid(thr, warmup=False, seed=seed)
+        torch.cuda.synchronize()
+        tmps.append(du["tmp"].view(K, C, G3).clone())
+        outs.append([getattr(m, f"density_grid_{i}").clone() for i in range(K)] +
+                    [getattr(m, f"density_bitfield_{i}").clone() for i in range(K)])
+        thr_dev = du["thr"].cpu().numpy()
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+    assert not torch.equal(tmps[0], tmps[2])
+    tmp = tmps[2]
+    hit = tmp > 0
+    e_u, e_uo = 1 - np.exp(-0.25), 1 - np.exp(-0.75)
+    for k in range(K):
+        for c in range(C):
+            h, o = hit[k, c], occ_mask[k, c]
+            f_free = float(h[~o].float().mean())
+            assert abs(f_free - e_u) < 0.01, (k, c, f_free)
+            if o.any():
+                f_occ = float(h[o].float().mean())
+                assert abs(f_occ - e_uo) < 0.01, (k, c, f_occ)
+    for k in range(K):
+        new = getattr(m, f"density_grid_{k}")
+        o = old[k]
+        assert torch.equal(new[o < 0], o[o < 0])
+        assert torch.equal(new[o >= 0], torch.maximum(o[o >= 0] * 0.95, tmp[k][o >= 0]))
+        g = new.double().cpu().numpy()
+        mean = g[g > 0].mean()
+        assert abs(thr_dev[k] - min(mean, thr)) <= 1e-5 * min(mean, thr), (thr_dev[k], mean)
+        bits = oracle.packbits(new.cpu().numpy().reshape(-1), float(thr_dev[k]))
+        assert np.array_equal(getattr(m, f"density_bitfield_{k}").cpu().numpy(), bits)
