@@ -32,6 +32,10 @@
 namespace {
 
 #define RT_WAVES 4
+#ifndef RT_MIN_BLOCKS
+#define RT_MIN_BLOCKS 1      // 2 waves per SIMD (146 VGPRs); 3 (min 2 blocks, 2x the grid) was
+                             // slower: 800x800 image 103 -> 111 ms (K 2), 113 -> 134 ms (K 4, scale 16)
+#endif
 
 // the wave's tile slots in LDS (march_ray_wave's emitting lanes write them)
 struct TileSink {
@@ -55,7 +59,7 @@ __device__ __forceinline__ float rd_lane(float v, int l) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
 }
 
-__global__ void __launch_bounds__(RT_WAVES * 64)
+__global__ void __launch_bounds__(RT_WAVES * 64, RT_MIN_BLOCKS)
 k_render_test(FieldArgs a, RenderArgs g) {
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FWD_FRAGS * RN_FRAG_HALFS];
     __shared__ LvTab sT;

@@ -5,16 +5,18 @@ from radnerf_amd import synthetic as S
 from radnerf_amd.networks import MNGP, Ray_Gate
 from radnerf_amd.rendering import ml_render
 dev = torch.device('cuda')
-K, scale = 2, 0.5
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+scale = float(sys.argv[2]) if len(sys.argv) > 2 else 0.5
 m = MNGP(scale, size=K, seed=3).to(dev); g = Ray_Gate(K, seed=4).to(dev)
+esf = 1 / 256 if scale > 0.5 else 0.0
 bits = S.bitfields(K, m.cascades, p=0.5, seed=1)
 with torch.no_grad():
     for i in range(K): getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
 o, d = (torch.from_numpy(a).to(dev) for a in S.rays(640000, scale, seed=99))
 with torch.no_grad():
-    r = ml_render(m, g, o, d, d, test_time=True)
+    r = ml_render(m, g, o, d, d, test_time=True, exp_step_factor=esf)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    r = ml_render(m, g, o, d, d, test_time=True)
+    r = ml_render(m, g, o, d, d, test_time=True, exp_step_factor=esf)
     torch.cuda.synchronize()
     print(json.dumps({"ms": (time.perf_counter() - t0) * 1e3, "total_samples": int(r.get("total_samples", 0)) if "total_samples" in r else None}))
