@@ -230,9 +230,8 @@ def main():
             ar.zero()
             r.train_step(rays_o, rays_d, rays_d, tgt, noises[i % 4], bg, 1e-3, 1e-2, 5e-2,
                          1e-4, esf, ar.views[0], ar.views[1], ar.views[2])
-            if world > 1:
-                ar.reduce(average=not args.pinned)
-            opt.step()
+            # all-reduce with Adam as its epilogue (one rank: plain Adam)
+            ar.reduce_and_step(opt, average=not args.pinned)
 
         for i in range(2):
             tstep(i)
@@ -253,7 +252,7 @@ def main():
             dist.all_reduce(tr_el, op=dist.ReduceOp.MAX)
         train = {"value": round(int(tr_acc) / float(tr_el) / 1e6, 2), "unit": "Msamples/s",
                  "ms_per_step": round(float(tr_el) / args.steps * 1e3, 4),
-                 "includes": "render + fused loss + backward + FusedAdam"}
+                 "includes": "render + fused loss + backward + (bucketed all-reduce with) FusedAdam"}
     # the same step through the drop-in path (rendering.ml_render: the
     # reference's op-by-op autograd structure, vren ops + field autograd on the
     # same kernels), for the callers that keep ml_rendering.py; rank 0 at N=1.

@@ -81,6 +81,40 @@ class GradAllReduce:
                 self.flat.div_(dist.get_world_size())
         return self.views
 
+    def reduce_and_step(self, opt, n_buckets=4, average=True):
+        """All-reduce + FusedAdam with the optimizer as the collective's
+        epilogue: the flat gradient goes out as
+        n_buckets asynchronous all-reduces, and each bucket's Adam update is
+        queued behind its own collective (work.wait() orders the compute
+        stream after it without blocking the host), so the updates of the
+        first buckets run while the last ones are still on the wire; the mean
+        over ranks is Adam's grad_scale (no division pass).  After the call
+        the gradient views hold the rank SUM.  One rank: opt.step()."""
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        if world == 1:
+            opt.step()
+            return self.views
+        n = self.flat.numel()
+        bounds = sorted({min(n, (n * i // n_buckets + 63) // 64 * 64) for i in range(n_buckets)}
+                        | {n})
+        if bounds[0] != 0:
+            bounds = [0] + bounds
+        ranges = list(zip(bounds[:-1], bounds[1:]))
+        works = [dist.all_reduce(self.flat[a:b], async_op=True) for a, b in ranges]
+        opt.begin_step()
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += p.numel()
+        for (a, b), w in zip(ranges, works):
+            w.wait()
+            for p, o in zip(self.params, offs):
+                lo, hi = max(a, o), min(b, o + p.numel())
+                if lo < hi:
+                    opt.update_range(p, lo - o, hi - o, 1.0 / world if average else 1.0)
+        opt.end_step()
+        return self.views
+
 
 def broadcast_buffers(module, src=0):
     """Keep density grids / bitfields identical across ranks."""

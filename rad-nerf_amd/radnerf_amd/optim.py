@@ -22,8 +22,21 @@ class FusedAdam(torch.optim.Optimizer):
     @torch.no_grad()
     def step(self, closure=None, grad_scale=1.0):
         loss = closure() if closure is not None else None
+        self.begin_step()
         for group in self.param_groups:
-            b1, b2 = group["betas"]
+            for p in group["params"]:
+                if p.grad is not None:
+                    self.update_range(p, 0, p.numel(), grad_scale)
+        self.end_step()
+        return loss
+
+    # The step in pieces, for an all-reduce epilogue (dist.GradAllReduce.
+    # reduce_and_step): the step counters advance once, then each gradient
+    # bucket's elements are updated as soon as its collective has landed.
+    @torch.no_grad()
+    def begin_step(self):
+        self._group_of = {}
+        for group in self.param_groups:
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -35,18 +48,34 @@ class FusedAdam(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p)
                     st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] += 1
-                g = p.grad.contiguous()
-                mirror = getattr(p, "_rn_f16", None)     # f16 copy kept by HashGridEncoding
-                lib().adam(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
-                           st["exp_avg_sq"].data_ptr(), p.numel(), float(group["lr"]), float(b1),
-                           float(b2), float(group["eps"]), int(st["step"]), float(grad_scale),
-                           None if mirror is None else mirror.data_ptr(),
-                           0 if mirror is None else p.numel(),
-                           torch.cuda.current_stream(p.device).cuda_stream)
-                # the kernel wrote p in place behind autograd's back: bump the
-                # epoch the modules' derived caches (f16 fragments) key on; the
-                # f16 table mirror was refreshed by the same pass
-                p._rn_epoch = getattr(p, "_rn_epoch", 0) + 1
-                if mirror is not None:
-                    p._rn_f16_key = (p._version, p._rn_epoch)
-        return loss
+                self._group_of[p] = group
+
+    @torch.no_grad()
+    def update_range(self, p, lo, hi, grad_scale=1.0):
+        """Adam on elements [lo, hi) of p (its gradient scaled by grad_scale)."""
+        if hi <= lo or p not in self._group_of:
+            return
+        group, st = self._group_of[p], self.state[p]
+        b1, b2 = group["betas"]
+        g = p.grad
+        if not g.is_contiguous():
+            raise RuntimeError("FusedAdam: contiguous gradients only")
+        mirror = getattr(p, "_rn_f16", None)     # f16 copy kept by HashGridEncoding
+        f4, f2 = 4 * lo, 2 * lo
+        lib().adam(p.data_ptr() + f4, g.data_ptr() + f4, st["exp_avg"].data_ptr() + f4,
+                   st["exp_avg_sq"].data_ptr() + f4, hi - lo, float(group["lr"]), float(b1),
+                   float(b2), float(group["eps"]), int(st["step"]), float(grad_scale),
+                   None if mirror is None else mirror.data_ptr() + f2,
+                   0 if mirror is None else hi - lo,
+                   torch.cuda.current_stream(p.device).cuda_stream)
+
+    @torch.no_grad()
+    def end_step(self):
+        for p in self._group_of:
+            # the kernel wrote p in place behind autograd's back: bump the
+            # epoch the modules' derived caches (f16 fragments) key on; the
+            # f16 table mirror was refreshed by the same pass
+            p._rn_epoch = getattr(p, "_rn_epoch", 0) + 1
+            if getattr(p, "_rn_f16", None) is not None:
+                p._rn_f16_key = (p._version, p._rn_epoch)
+        self._group_of = {}

@@ -25,7 +25,8 @@ MAX_SAMPLES = 1024
 class Trainer:
     def __init__(self, model, gating_net, n_rays, lr=1e-2, lambda_opacity=1e-3,
                  lambda_cv_importance=0.0, lambda_depth_mutual=0.0, exp_step_factor=None,
-                 random_bg=False, update_interval=16, warmup_steps=256, seed=0):
+                 random_bg=False, update_interval=16, warmup_steps=256, seed=0,
+                 bucketed=True):
         self.model, self.gate = model, gating_net
         self.device = model.mlp_params.device
         self.renderer = FusedMLRenderer(model, gating_net, n_rays)
@@ -43,6 +44,9 @@ class Trainer:
             p.grad = v
         self.opt = FusedAdam(params, lr=lr, eps=1e-15)      # train_ml.py:143
         self.update_interval, self.warmup_steps, self.seed = update_interval, warmup_steps, seed
+        # Adam as the epilogue of a bucketed all-reduce (dist.GradAllReduce.
+        # reduce_and_step); False: one collective, a division, then Adam
+        self.bucketed = bucketed
         self.global_step = 0
 
     def _bg(self):
@@ -69,7 +73,10 @@ class Trainer:
         terms, _ = self.renderer.train_step(rays_o, rays_d, second, target_rgb, noise, self._bg(),
                                             exp_step_factor=self.esf, grid_grad=v[0],
                                             mlp_grad=v[1], gate_grad=v[2], **self.lambdas)
-        self.grads.reduce()
-        self.opt.step()
+        if self.bucketed:
+            self.grads.reduce_and_step(self.opt)
+        else:
+            self.grads.reduce()
+            self.opt.step()
         self.global_step += 1
         return terms

@@ -19,6 +19,26 @@ def _free_port():
     return p
 
 
+class _RecordingOpt:
+    """Stands in for FusedAdam (a GPU kernel) in the epilogue test: records
+    the ranges it is asked to update and the gradient they held then."""
+    def __init__(self):
+        self.calls, self.snap, self.began, self.ended = [], {}, False, False
+
+    def begin_step(self):
+        self.began = True
+
+    def update_range(self, p, lo, hi, grad_scale=1.0):
+        self.calls.append((p, lo, hi, grad_scale))
+        self.snap[(id(p), lo)] = p.grad.view(-1)[lo:hi].clone()
+
+    def end_step(self):
+        self.ended = True
+
+    def step(self):
+        raise AssertionError("world > 1 goes through the epilogue")
+
+
 def _worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -49,7 +69,27 @@ def _worker(rank, world, port, q):
         got = [torch.zeros_like(draw) for _ in range(world)]
         dist.all_gather(got, draw)
         ok_stream = all(torch.equal(x, draw) for x in got) and not torch.equal(draw, other)
-        q.put((rank, lo, hi, ok_mean, ok_bcast and ok_stream))
+        # bucketed all-reduce with the optimizer as its epilogue: every element
+        # updated exactly once, from its bucket's summed gradient, at scale 1/world
+        params2 = [torch.zeros(1000), torch.zeros(37), torch.zeros(5)]
+        ar2 = rdist.GradAllReduce(params2, "cpu")
+        for p_, v in zip(params2, ar2.views):
+            p_.grad = v
+        for i, v in enumerate(ar2.views):
+            v.copy_(torch.arange(v.numel(), dtype=torch.float32) * (rank + 1) + i)
+        opt = _RecordingOpt()
+        ar2.reduce_and_step(opt, n_buckets=4)
+        ok_epi = opt.began and opt.ended and len(opt.calls) > 3
+        for p_, v in zip(params2, ar2.views):
+            seen = torch.zeros(p_.numel())
+            for q_, lo_, hi_, sc in opt.calls:
+                if q_ is p_:
+                    seen[lo_:hi_] += 1
+                    ok_epi = ok_epi and sc == 1.0 / world
+                    # the bucket's sum had landed when its update was queued
+                    ok_epi = ok_epi and torch.equal(opt.snap[(id(q_), lo_)], v[lo_:hi_])
+            ok_epi = ok_epi and bool((seen == 1).all())
+        q.put((rank, lo, hi, ok_mean, ok_bcast and ok_stream and ok_epi))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put((rank, "error", repr(e), False, False))

@@ -25,14 +25,14 @@ def _port():
     return p
 
 
-def _run_ranks(worker, out, timeout=100):
+def _run_ranks(worker, out, timeout=100, extra=()):
     port = _port()
     procs = []
     for rank in range(2):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                    LOCAL_RANK=str(rank), WORLD_SIZE="2")
         procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", worker),
-                                       str(out)], env=env, stdout=subprocess.PIPE,
+                                       str(out), *extra], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT))
     logs = []
     for p in procs:
@@ -69,3 +69,17 @@ def test_data_parallel_training_stays_identical(tmp_path):
     assert all(res["identical"].values()), res["identical"]
     assert all(res["bitfields_changed"]), res
     assert res["finite"]
+
+
+def test_bucketed_adam_epilogue_matches_plain(tmp_path):
+    """GradAllReduce.reduce_and_step (4 asynchronous all-reduce buckets, each
+    bucket's FusedAdam update queued behind its collective, the 1/world mean
+    as Adam's grad_scale) vs reduce() (one collective + division) +
+    FusedAdam.step(), on identical per-rank gradients, 3 steps, buckets cutting
+    across parameters: bit-identical parameters and moments on both ranks
+    (world = 2: the division by 2 and the scale by 1/2 are both exact)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks("adam_worker.py", tmp_path / "adam.json", timeout=100)
+    assert res["world"] == 2
+    assert res["same_params"] and res["same_moments"] and res["ranks_agree"], res
