@@ -162,6 +162,16 @@ class FusedMLRenderer:
         # (K = 1, 8192 rays) 512 = 1024 (tools/step_variants.py, r02)
         rk = n_rays * model.size
         self.max_chunk = 256 if rk <= 1024 else (512 if rk <= 4096 else 1024)
+        # with the fixed-point scatter (cheaper requests) longer chunks pay at
+        # scale 0.5 with several sub-NeRFs (fewer end-of-chunk ring flushes):
+        # C3 step 1024 5.02, 1280 4.94, 1536 4.89, 1792 4.92 ms; K = 8 at
+        # scale 16 (C5 per GPU) 1024 12.36, 2048 12.23 ms; K = 4 at scale 16
+        # (C4 per GPU) keeps 1024 (3.82 vs 3.92 at 1536); K = 1 (C2) 512-1024
+        # within 0.6 % (tools/step_variants.py, profiles/r02/step_variants_fx_chunk.json)
+        if model.size >= 8 and rk > 4096:
+            self.max_chunk = 2048
+        elif model.size >= 2 and rk > 4096 and float(model.scale) <= 0.5:
+            self.max_chunk = 1536
         # exact integer accumulation of the grid gradient (rn_seed_scale +
         # returning u32 atomics with carries + rn_igrad_to_f32): bitwise
         # reproducible grid gradients, but each issue waits for the previous

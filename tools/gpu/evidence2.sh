@@ -17,7 +17,6 @@ timeout -k 10 700 python -u -m pytest tests -m gpu -q -p no:cacheprovider --time
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/tests_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
-timeout -k 10 500 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0 --test-time-rays 0"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py $Q --steps 10 --warmup 3 > gpurun_out/prof_$TAG.log 2>&1 || exit $?
 cp profiles/traffic.json gpurun_out/traffic.json
@@ -31,6 +30,8 @@ pmc() {   # $1 = name, rest = bench args
 pmc c3 || exit $?
 pmc c4 --models 4 --scale 16 --rays 4096 || exit $?
 pmc c5 --models 8 --scale 16 --rays 8192 || exit $?
+# the headline line (with the CPU baseline) against this code's own PMC figures
+timeout -k 10 500 python bench.py --traffic-json gpurun_out/traffic.json > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || exit $?
 # the C4 / C5 per-GPU shapes with their own PMC figures (not the headline)
 timeout -k 10 300 python bench.py --models 4 --scale 16 --rays 4096 --cpu-rays 0 --dropin-step 0 --traffic-json gpurun_out/traffic.json > gpurun_out/bench_c4_$TAG.json 2> gpurun_out/bench_c4_$TAG.err || exit $?
 timeout -k 10 300 python bench.py --models 8 --scale 16 --rays 8192 --cpu-rays 0 --dropin-step 0 --traffic-json gpurun_out/traffic.json > gpurun_out/bench_c5_$TAG.json 2> gpurun_out/bench_c5_$TAG.err || exit $?

@@ -2,7 +2,7 @@
 fwd+bwd steps with no per-launch events, variants interleaved round by round
 (rule 24 of cdna_hip_programming.md §5.4); prints median ms per step.
 
-usage: [STEP_K=K] [STEP_B=B] python tools/step_variants.py [attr=value[,attr=value]] ...
+usage: [STEP_K=K] [STEP_B=B] [STEP_SCALE=S] python tools/step_variants.py [attr=value[,attr=value]] ...
   e.g. gate_bwd_at=field gate_bwd_at=early gate_bwd_at=main
 """
 import json
@@ -32,16 +32,18 @@ def main():
     variants = sys.argv[1:] or ["gate_bwd_at=field", "gate_bwd_at=early", "gate_bwd_at=main"]
     dev = torch.device("cuda")
     B, K, steps = int(os.environ.get("STEP_B", 8192)), int(os.environ.get("STEP_K", 2)), 10
-    m = MNGP(0.5, size=K, seed=3).to(dev)
+    scale = float(os.environ.get("STEP_SCALE", 0.5))
+    esf = 1.0 / 256 if scale > 0.5 else 0.0
+    m = MNGP(scale, size=K, seed=3).to(dev)
     g = Ray_Gate(K, seed=4).to(dev)
-    bits = S.bitfields(K, 1, p=0.5, seed=1)
+    bits = S.bitfields(K, m.cascades, p=0.5, seed=1)
     with torch.no_grad():
         for i in range(K):
             getattr(m, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
-    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B, 0.5, seed=0))
+    o, d = (torch.from_numpy(a).to(dev) for a in S.rays(B, scale, seed=0))
     nz = torch.from_numpy(S.noise(K, B, seed=2)).to(dev)
     sd = [torch.from_numpy(a).to(dev) for a in S.loss_seeds(B, K, seed=4)]
-    bg = torch.ones(3, device=dev)
+    bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
     r = FusedMLRenderer(m, g, B)
     gg = torch.zeros_like(m.xyz_encoder.params)
     mg = torch.zeros_like(m.mlp_params)
@@ -49,7 +51,7 @@ def main():
     defaults = {k: getattr(r, k) for v in variants for k in parse(v)}
 
     def step():
-        _, _, _, gt, _ = r.forward(o, d, d, nz, bg)
+        _, _, _, gt, _ = r.forward(o, d, d, nz, bg, 1e-4, esf)
         r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
 
     times = {v: [] for v in variants}
