@@ -202,7 +202,7 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * per model, read by the merged kernels with one 80-B load per ticket).  cap_chunks must bound the chunk
  * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2.
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
- * stages 144-B rows in its scratch slice (scratch: blocks x scratch_rows x 36
+ * stages 80-B rows in its scratch slice (scratch: blocks x scratch_rows x 20
  * f32, scratch_rows >= max_chunk + n_models * max_samples) and parks per-model
  * dW accumulators in park (blocks x n_models x 16384 f32).
  * Replaces, with rn_field_bwd, the backward of the tcnn modules called at

@@ -868,7 +868,11 @@ k_field_bwd(FieldArgs a) {
 // The grid gradient is the same sum as k_field_bwd's (float atomics: equal up
 // to summation order); dW is identical per model.
 // ---------------------------------------------------------------------------
-#define MB_ROW 36          // scratch row floats: dE[32] | ux uy uz | pad
+// scratch row (80 B = 20 floats): dE[32] as f16 in the block iteration's
+// gradient scale (the dX chain's own range; tcnn's dL/dencoding is f16 too) |
+// ux uy uz | 1 / scale (fp32).  Half the 144 B of fp32 rows: the chunk's rows
+// stay in L2 for longer chunks.
+#define MB_ROW 20
 #define CH_DESC 20         // chunk descriptor ints (80 B, 16-B aligned)
 #define MB_KMAX 8
 
@@ -1025,13 +1029,13 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 if (valid) {
                     const float ginv = zero_iter ? 0.f : 1.0f / gscale;
                     float* row = rows + (size_t)(roff + i) * MB_ROW;
+                    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+                    h4* rh = reinterpret_cast<h4*>(row);
 #pragma unroll
-                    for (int g = 0; g < 4; ++g) {   // features 8g + 4h .. +3 = dE[4g .. 4g+3]
-                        *reinterpret_cast<float4*>(row + 8 * g + 4 * h) =
-                            make_float4(dE[4 * g] * ginv, dE[4 * g + 1] * ginv,
-                                        dE[4 * g + 2] * ginv, dE[4 * g + 3] * ginv);
-                    }
-                    if (h == 0) *reinterpret_cast<float4*>(row + 32) = make_float4(ux, uy, uz, 0.f);
+                    for (int g = 0; g < 4; ++g)     // features 8g + 4h .. +3 = dE[4g .. 4g+3]
+                        rh[2 * g + h] = h4{(_Float16)dE[4 * g], (_Float16)dE[4 * g + 1],
+                                           (_Float16)dE[4 * g + 2], (_Float16)dE[4 * g + 3]};
+                    if (h == 0) *reinterpret_cast<float4*>(row + 16) = make_float4(ux, uy, uz, ginv);
                 }
             }
         }
@@ -1061,21 +1065,22 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
                 // rows were written by other waves of this block: read past L1 (nt)
                 typedef float nf4 __attribute__((ext_vector_type(4)));
-                const nf4* src = reinterpret_cast<const nf4*>(rows + (size_t)row_i * MB_ROW)
-                                 + 4 * half;
+                typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+                const float* rw = rows + (size_t)row_i * MB_ROW;
+                const nf4 u = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(rw) + 4);
+                const h8* src = reinterpret_cast<const h8*>(rw) + 2 * half;
                 float* dst = sG + j * SG_STRIDE + 16 * half;
 #pragma unroll
-                for (int qq = 0; qq < 4; ++qq) {
-                    const nf4 v = __builtin_nontemporal_load(src + qq);
-                    *reinterpret_cast<float2*>(dst + 4 * qq) = make_float2(v.x, v.y);
-                    *reinterpret_cast<float2*>(dst + 4 * qq + 2) = make_float2(v.z, v.w);
-                    nz |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
+                for (int qq = 0; qq < 2; ++qq) {
+                    const h8 v = __builtin_nontemporal_load(src + qq);
+#pragma unroll
+                    for (int e2 = 0; e2 < 8; e2 += 2) {
+                        const float a0 = (float)v[e2] * u.w, a1 = (float)v[e2 + 1] * u.w;
+                        *reinterpret_cast<float2*>(dst + 8 * qq + e2) = make_float2(a0, a1);
+                        nz |= (a0 != 0.f) | (a1 != 0.f);
+                    }
                 }
-                if (half) {
-                    const nf4 u = __builtin_nontemporal_load(
-                        reinterpret_cast<const nf4*>(rows + (size_t)row_i * MB_ROW) + 8);
-                    *reinterpret_cast<nf4*>(sU + j * 4) = u;
-                }
+                if (half) *reinterpret_cast<nf4*>(sU + j * 4) = u;
             }
             // a window whose rows are all zero (rays past early termination)
             // adds nothing; skipping it keeps the walk state valid (entries

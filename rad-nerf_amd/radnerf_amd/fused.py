@@ -94,7 +94,7 @@ class Workspace:
         key = (blocks, rows)
         if self._bwd_scratch is None or self._bwd_scratch[0] != key:
             f = dict(device=self.device, dtype=torch.float32)
-            self._bwd_scratch = (key, torch.empty(blocks * rows * 36, **f),
+            self._bwd_scratch = (key, torch.empty(blocks * rows * 20, **f),
                                  torch.empty(blocks * self.K * 8 * 2048, **f))
         return rows, self._bwd_scratch[1], self._bwd_scratch[2]
 

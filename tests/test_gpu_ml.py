@@ -267,11 +267,14 @@ def _merged_vs_split(cuda, B, K, scale, p=0.5):
                                        (512, 8, 0.5)])
 def test_merged_backward_matches_per_model(cuda, B, K, scale):
     """rn_field_bwd_merged (K models' grid gradients scattered merged per ray)
-    vs rn_field_bwd (one model per block): the same sums in another order."""
+    vs rn_field_bwd (one model per block): the same sums in another order; the
+    merged kernel stages dL/dencoding as f16 in the block's gradient scale
+    (as tcnn's f16 dL/dencoding), so its grid gradient is within f16 rounding
+    (measured 9.4e-5) and the MLP / gate gradients agree to summation order."""
     r, (gm, gs) = _merged_vs_split(cuda, B, K, scale)
-    for a, b in zip(gm, gs):
+    for i, (a, b) in enumerate(zip(gm, gs)):
         rel = (a - b).norm() / b.norm().clamp_min(1e-30)
-        assert rel <= 1e-5, rel
+        assert rel <= (3e-4 if i == 0 else 1e-5), (i, rel)
     # merged order: ray-major, then t, ties by model (bit-exact)
     w = r.ws
     cnt = w.counts.cpu().numpy().astype(np.int64)
@@ -378,9 +381,9 @@ def test_merged_backward_edge_occupancy(cuda, p, K):
     (odd model count, many 1024-capped rays): merged = per-model backward."""
     B = 256
     r, (gm, gs) = _merged_vs_split(cuda, B, K, 0.5, p=p)
-    for a, b in zip(gm, gs):
+    for i, (a, b) in enumerate(zip(gm, gs)):
         rel = (a - b).norm() / b.norm().clamp_min(1e-30)
-        assert rel <= 1e-5, rel
+        assert rel <= (3e-4 if i == 0 else 1e-5), (i, rel)     # f16-staged dE (merged)
     if p == 0.0:
         assert int(r.ws.meta[1]) == 0
         assert float(gm[0].abs().max()) == 0.0
