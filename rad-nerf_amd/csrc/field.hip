@@ -227,7 +227,7 @@ __device__ __forceinline__ void grid_walk_window(const FieldArgs& a, const LvTab
             const vf2 gc = gn;
             const int nx = s_base + (j + 1 < nq ? j + 1 : 0);
             un = *(lds_cf4*)(sU + nx * 4);
-            gn = *(lds_cf2*)(gcol + nx * SG_STRIDE);
+            gn = *(lds_cf2*)(gcol + __umul24((uint32_t)nx, SG_STRIDE));   // u32 offset, not a u64 mad
             const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
             // this class's corner of the cell: the one of {g, g+1} with parity p
             const uint32_t cx = (px ^ p.gx) & 1u, cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
@@ -438,17 +438,20 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
 // lane-major (a lane's even-X and odd-X records adjacent: they share a 64-B
 // segment, so an instruction boundary splits them less often; replay of the
 // bench samples, tools/atomic_sim2.py: 15.18 -> 14.65 requests/sample)
-__device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint64_t smask,
-                                           uint32_t lvl_off) {
-    const uint64_t m0 = __builtin_amdgcn_ballot_w64(e0) & smask;
-    const uint64_t m1 = __builtin_amdgcn_ballot_w64(e1) & smask;
+__device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t lvl_off) {
+    // a stream's 4 lanes are one DPP quad: the lane's first record index is
+    // the exclusive quad prefix of the per-lane record counts (two quad_perm
+    // steps), the stream's total its lane 3 (ballot + mbcnt + popcount per
+    // mask took ~19 VALU operations per step, this ~10; same order)
     const int s = rn_lane() >> 2;
+    const uint32_t q = rn_lane() & 3;
+    const uint32_t x = (e0 ? 1u : 0u) + (e1 ? 1u : 0u);
+    const uint32_t m1 = q >= 1u ? ~0u : 0u, m2 = q >= 2u ? ~0u : 0u;      // loop-invariant
+    uint32_t t = x + ((uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x90, 0xf, 0xf, true) & m1);  // [0,0,1,2]
+    t += (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0x40, 0xf, 0xf, true) & m2;         // [0,0,0,1]
+    const uint32_t pushed = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0xff, 0xf, 0xf, true);  // [3,3,3,3]
+    const uint32_t below = t - x;
     uint32_t* base = W.ring + s * 3 * W2_RING;
-    // records of the stream's lower lanes
-    const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u)) +
-                           __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
     if (e0) {
         const uint32_t rec = w2_wrap(W.tail + below);
         base[rec] = 8u * (lvl_off + W.cur0);
@@ -461,7 +464,6 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint64_t 
         base[W2_RING + rec] = __float_as_uint(W.a10);
         base[2 * W2_RING + rec] = __float_as_uint(W.a11);
     }
-    const uint32_t pushed = (uint32_t)(__builtin_popcountll(m0) + __builtin_popcountll(m1));
     W.tail = w2_wrap(W.tail + pushed);
     W.pend += pushed;
 }
@@ -485,7 +487,6 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
     const int stream = lane >> 2, eighth = stream >> 1;
     const uint32_t py = lane & 1, pz = (lane >> 1) & 1;
     const LvConst lc = walk2_level(a, sT);
-    const uint64_t smask = 0xfull << (4 * stream);
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
     lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - wid) : wid);
     const int s_base = eighth * 32;
@@ -501,7 +502,7 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
         const vf2 gc = gn;
         const int nx = s_base + (j + 1 < ne ? j + 1 : 0);
         un = *(lds_cf4*)(sU + nx * 4);
-        gn = *(lds_cf2*)(gcol + nx * SG_STRIDE);
+        gn = *(lds_cf2*)(gcol + __umul24((uint32_t)nx, SG_STRIDE));   // u32 offset, not a u64 mad
         const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
         const uint32_t c0 = p.gx & 1u;                    // x offset of the even-X corner
         const uint32_t cy = (py ^ p.gy) & 1u, cz = (pz ^ p.gz) & 1u;
@@ -514,7 +515,7 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
         const bool row = Y == W.ey && Z == W.ez;
         const bool same0 = row && X0 == W.ex0, same1 = row && X1 == W.ex1;
         walk2_push(W, act && !same0 && W.ex0 != W2_NONE, act && !same1 && W.ex1 != W2_NONE,
-                   smask, lc.off);
+                   lc.off);
         if (act) {
             W.a00 = (same0 ? W.a00 : 0.f) + w0 * gc.x;
             W.a01 = (same0 ? W.a01 : 0.f) + w0 * gc.y;
@@ -541,8 +542,7 @@ __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
                                           __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                           Walk2& W, int dbg) {
     const LvConst lc = walk2_level(a, sT);
-    const uint64_t smask = 0xfull << (4 * (rn_lane() >> 2));
-    walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, smask, lc.off);
+    walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, lc.off);
     walk2_drain<GM>(W, 0u, grad_rs, G, dbg);
     if (GM == 1) walk2_settle(W, G);
     walk2_begin(W, W.ring);
