@@ -419,10 +419,12 @@ template <int GM>
 __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
-    const bool lead = (rn_lane() & 3) == 0;
+    const uint32_t need = min_cnt > 1u ? min_cnt : 1u;
     for (;;) {
         const uint32_t pend = W.pend;
-        uint64_t m = __builtin_amdgcn_ballot_w64(lead && pend > 0u && pend >= min_cnt);
+        // lane 0 of each stream's quad (a plain compare's ballot: no
+        // bool -> mask round trip)
+        uint64_t m = __builtin_amdgcn_ballot_w64(pend >= need) & 0x1111111111111111ull;
         if (!m) break;
         while (m) {
             const int s = __builtin_ctzll(m) >> 2;

@@ -2,7 +2,7 @@
 # A/B of two builds of librn.so on one box (dev tool): the field-kernel GPU
 # tests on the new build, then the headline bench and the C5 per-GPU shape
 # alternating old / new (RADNERF_LIB), so both see the same card and clocks.
-# usage: tools/gpu/ab.sh <tag> [old_lib]
+# usage: tools/gpu/ab.sh <tag> [old_lib]   (VARIANTS="old new b": librn_<v>.so, new = librn.so)
 set -u
 mkdir -p gpurun_out
 TAG=${1:-ab}
@@ -13,8 +13,8 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_fx.py tests/test_gpu_ml.py 
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/tests_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 for r in 1 2; do
-  for v in old new; do
-    L=$OLD; [ $v = new ] && L=$NEW
+  for v in ${VARIANTS:-old new}; do
+    L=rad-nerf_amd/radnerf_amd/librn_$v.so; [ $v = old ] && L=$OLD; [ $v = new ] && L=$NEW
     RADNERF_LIB=$L timeout -k 10 200 python bench.py $Q --steps 40 --warmup 5 > gpurun_out/ab_${TAG}_c3_${v}_$r.json 2> gpurun_out/ab_${TAG}_c3_${v}_$r.err || exit $?
     RADNERF_LIB=$L timeout -k 10 200 python bench.py $Q --steps 20 --warmup 3 --models 8 --scale 16 --rays 8192 > gpurun_out/ab_${TAG}_c5_${v}_$r.json 2> gpurun_out/ab_${TAG}_c5_${v}_$r.err || exit $?
   done
