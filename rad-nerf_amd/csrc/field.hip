@@ -1019,7 +1019,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 rn_lds_order();
                 const int i = w0 + wid * 32 + c;
                 const bool valid = i < n_k;
-                const int64_t s = a_k + (valid ? i : 0);
+                // ablation 256: every tile reads the chunk's first 32 samples
+                // (cache-resident inputs; timing only)
+                const int64_t s = a_k + (valid ? ((dbg & 256) ? (i & 31) : i) : 0);
                 FwdState st;
                 float ux, uy, uz;
                 tile_forward_s<1, CACHE>(a, sT, sW, s, valid,
