@@ -454,18 +454,18 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t 
     const uint32_t pushed = (uint32_t)__builtin_amdgcn_mov_dpp((int)t, 0xff, 0xf, 0xf, true);  // [3,3,3,3]
     const uint32_t below = t - x;
     uint32_t* base = W.ring + s * 3 * W2_RING;
-    if (e0) {
-        const uint32_t rec = w2_wrap(W.tail + below);
-        base[rec] = 8u * (lvl_off + W.cur0);
-        base[W2_RING + rec] = __float_as_uint(W.a00);
-        base[2 * W2_RING + rec] = __float_as_uint(W.a01);
-    }
-    if (e1) {
-        const uint32_t rec = w2_wrap(W.tail + below + (e0 ? 1u : 0u));
-        base[rec] = 8u * (lvl_off + W.cur1);
-        base[W2_RING + rec] = __float_as_uint(W.a10);
-        base[2 * W2_RING + rec] = __float_as_uint(W.a11);
-    }
+    // branch-free: a lane with nothing to emit writes the stream's free slot
+    // tail + pushed (pending records are <= 31 before the push and <= 39
+    // after it, so that slot is outside [head, tail + pushed) of a 40-slot
+    // ring; it is overwritten before it is ever read)
+    const uint32_t r0 = w2_wrap(W.tail + (e0 ? below : pushed));
+    const uint32_t r1 = w2_wrap(W.tail + (e1 ? below + (e0 ? 1u : 0u) : pushed));
+    base[r0] = 8u * (lvl_off + W.cur0);
+    base[W2_RING + r0] = __float_as_uint(W.a00);
+    base[2 * W2_RING + r0] = __float_as_uint(W.a01);
+    base[r1] = 8u * (lvl_off + W.cur1);
+    base[W2_RING + r1] = __float_as_uint(W.a10);
+    base[2 * W2_RING + r1] = __float_as_uint(W.a11);
     W.tail = w2_wrap(W.tail + pushed);
     W.pend += pushed;
 }
