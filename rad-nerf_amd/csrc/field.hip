@@ -498,8 +498,13 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
     typedef __attribute__((address_space(3))) const vf2 lds_cf2;
     vf4 un = *(lds_cf4*)(sU + s_base * 4);
     vf2 gn = *(lds_cf2*)(gcol + s_base * SG_STRIDE);
-    for (int j = 0; j < n0; ++j) {                        // wave-uniform trip count
-        const bool act = j < ne;
+    // steps below the wave's smallest count need no per-lane activity test
+    // (no exec-mask region): all but a chunk's last window run that form
+    int nmin = ne;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) nmin = min(nmin, __shfl_xor(nmin, off));
+    auto step = [&](int j, auto check) {
+        const bool act = decltype(check)::value ? j < ne : true;
         const vf4 uc = un;
         const vf2 gc = gn;
         const int nx = s_base + (j + 1 < ne ? j + 1 : 0);
@@ -535,7 +540,10 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
             W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
         }
         walk2_drain<GM>(W, 32u, grad_rs, G, dbg);
-    }
+    };
+    int j = 0;                                            // wave-uniform trip counts
+    for (; j < nmin; ++j) step(j, std::integral_constant<bool, false>{});
+    for (; j < n0; ++j) step(j, std::integral_constant<bool, true>{});
 }
 
 // end of a chunk: emit every live entry and drain the rings completely
