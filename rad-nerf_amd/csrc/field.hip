@@ -348,7 +348,8 @@ struct FxGrad {
 __device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? v - W2_RING : v; }
 
 // issue up to 32 records of stream s (wave-uniform) as one atomic instruction
-template <int GM>
+// (FULL: exactly 32, every lane issues: no exec-mask region)
+template <int GM, bool FULL = false>
 __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
@@ -364,7 +365,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         W.oldA = W.oldB; W.loA = W.loB; W.hiA = W.hiB; W.offA = W.offB;
         W.oldB = 0; W.loB = 0; W.hiB = 0;
     }
-    if ((uint32_t)lane < 2u * cnt) {
+    if (FULL || (uint32_t)lane < 2u * cnt) {
         const uint32_t rec = w2_wrap(h + (lane >> 1));
         const uint32_t* base = W.ring + s * 3 * W2_RING;
         const uint32_t off = base[rec] + 4u * (lane & 1);
@@ -404,7 +405,9 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         }
     }
     asm volatile("" ::: "memory");
-    if ((lane >> 2) == s) { W.head = w2_wrap(W.head + cnt); W.pend -= cnt; }
+    const bool me = (lane >> 2) == s;                     // selects, not a branch
+    W.head = me ? w2_wrap(W.head + cnt) : W.head;
+    W.pend = me ? W.pend - cnt : W.pend;
 }
 
 // integer mode: settle the two outstanding issues (end of a chunk)
@@ -429,7 +432,10 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
         while (m) {
             const int s = __builtin_ctzll(m) >> 2;
             const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
-            walk2_issue<GM>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
+            if (min_cnt >= 32u)     // threshold drain (constant after inlining): p >= 32
+                walk2_issue<GM, true>(W, s, 32u, grad_rs, G, dbg);
+            else
+                walk2_issue<GM>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
             m &= m - 1;
         }
         if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
