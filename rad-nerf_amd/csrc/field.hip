@@ -357,7 +357,14 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
     // the stream's level: even streams level wid, odd 15 - wid (scalar)
     const bool odd = s & 1;
-    const float sc_s = GM >= 2 ? (odd ? W.fxB : W.fxA) : 0.f;
+    // the level's scale as float bits selected on the scalar unit (gfx9 has
+    // no scalar float compare: a float test here became a VALU compare + vcc
+    // branch per issue)
+    const uint32_t scb = GM >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane(
+                                       (int)(odd ? __float_as_uint(W.fxB) : __float_as_uint(W.fxA)))
+                                 : 0u;
+    const bool fx_lvl = (scb << 1) != 0u;       // 2^e_l > 0: fixed point; +-0: fp32 atomics
+    const float sc_s = __uint_as_float(scb);
     asm volatile("" ::: "memory");
     if (GM == 1) {
         // the issue two back has had a whole issue's time to return
@@ -372,12 +379,12 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
         if (dbg & 1) {
             asm volatile("" :: "v"(off), "v"(v));
-        } else if (GM == 3 && sc_s == 0.f) {
+        } else if (GM == 3 && !fx_lvl) {
             // redo: this level went in with fp32 atomics in the first pass
         } else if (dbg & 64) {      // ablation: non-returning i32 adds (timing only)
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
                 (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
-        } else if (GM == 2 && sc_s != 0.f) {
+        } else if (GM == 2 && fx_lvl) {
             const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             // 2^e_l is a power of two: v * sc is exact; v_cvt_i32_f32 saturates
@@ -509,6 +516,10 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
     int nmin = ne;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) nmin = min(nmin, __shfl_xor(nmin, off));
+    // both bounds in SGPRs: scalar loops (a VGPR bound made the compiler run
+    // them as divergent loops with exec-mask bookkeeping every step)
+    nmin = __builtin_amdgcn_readfirstlane(nmin);
+    n0 = __builtin_amdgcn_readfirstlane(n0);
     auto step = [&](int j, auto check) {
         const bool act = decltype(check)::value ? j < ne : true;
         const vf4 uc = un;
