@@ -15,10 +15,17 @@ the metric definition.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+`--gpus N` without a torchrun environment starts the N ranks itself (a
+`torch.distributed.run` child process, before this process touches the GPU)
+and exits with its status; under torchrun every rank checks that the world
+size equals --gpus and the JSON line reports the ranks it saw.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,6 +57,20 @@ ATOMIC_PEAK_GREQ = 1.3e12 / 64 / 1e9
 # (tools/atomic_probe.hip, profiles/r01/atomic_probe.json); the guide gives no
 # integer figure
 ATOMIC_U32_PEAK_GREQ = 26.6
+
+
+# BASELINE.json configs by (sub-NeRFs, scale): C1/C2 single NGP (C1 is the
+# reference's CPU case at 1024 rays), C3 K=2, C4 K=4 scale 16, C5 K=8 scale 16
+def config_label(K, scale, rays):
+    if K == 1:
+        return "C1" if rays <= 1024 else "C2"
+    if K == 2 and scale <= 0.5:
+        return "C3"
+    if K == 4 and scale >= 16:
+        return "C4"
+    if K == 8 and scale >= 16:
+        return "C5"
+    return "custom"
 
 
 def workload_key(K, scale, rays, occupancy):
@@ -96,17 +117,81 @@ def parse():
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
                          "multi-rank path on one GPU")
+    ap.add_argument("--buckets", type=int, default=4,
+                    help="N>1: the gradient all-reduce as this many asynchronous bucket "
+                         "collectives, each averaged behind its own wait (1 = one collective)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, check the world size, print the ranks seen and exit "
+                         "(no GPU work; with --backend gloo it runs on CPU)")
     return ap.parse_args()
+
+
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def self_launch(args):
+    """--gpus N > 1 with no torchrun environment: run this script under
+    torch.distributed.run with N ranks (one process per GPU) as a child
+    process and return its exit status; None when this process is a rank
+    (or N = 1).  Runs before anything initialises the GPU in this process."""
+    if args.gpus <= 1 or "WORLD_SIZE" in os.environ:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def ranks_seen(rank, local, world, backend, dev_index):
+    """(rank, local rank, host, device) of every rank, gathered on all ranks."""
+    me = {"rank": rank, "local_rank": local, "host": socket.gethostname(), "device": dev_index}
+    if world == 1:
+        return [me]
+    out = [None] * world
+    dist.all_gather_object(out, me)
+    return out
+
+
+def check_world(args, world):
+    if world != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} but the process group has {world} "
+                         f"rank(s)\n")
+        sys.exit(3)
+
+
+def launch_check(args, rank, local, world):
+    """--launch-check: the launcher's contract without GPU work."""
+    check_world(args, world)
+    seen = ranks_seen(rank, local, world, None, None)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": world,
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "ranks_seen": seen}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
     args = parse()
+    rc = self_launch(args)
+    if rc is not None:
+        sys.exit(rc)
     from radnerf_amd import dist as rdist
     from radnerf_amd import synthetic as S
     from radnerf_amd.fused import FusedMLRenderer
     from radnerf_amd.networks import MNGP, Ray_Gate
 
-    rank, local, world = rdist.init(backend=None if args.backend == "auto" else args.backend)
+    backend = None if args.backend == "auto" else args.backend
+    if args.launch_check:
+        rank, local, world = rdist.init(backend=backend or "gloo")
+        return launch_check(args, rank, local, world)
+    rank, local, world = rdist.init(backend=backend)
+    check_world(args, world)
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
     local = rdist.device_index(local)
@@ -115,7 +200,12 @@ def main():
     B, K, scale = args.rays, args.models, args.scale
     esf = 1.0 / 256 if scale > 0.5 else 0.0
 
-    model = MNGP(scale, size=K, seed=3).to(dev)
+    if K == 1:
+        # single NGP (C1 / C2): the model render() takes (density_bitfield)
+        from radnerf_amd.networks import NGP
+        model = NGP(scale, seed=3).to(dev)
+    else:
+        model = MNGP(scale, size=K, seed=3).to(dev)
     gate = Ray_Gate(K, seed=4).to(dev)
     bits = S.bitfields(K, model.cascades, p=args.occupancy, seed=1)
     with torch.no_grad():
@@ -150,7 +240,9 @@ def main():
         r.backward(rays_o, rays_d, rays_d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4,
                    grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
         if world > 1:
-            ar.reduce(average=not args.pinned)   # pinned: partial gradients add up
+            # bucketed asynchronous all-reduce, each bucket averaged behind its
+            # own wait (pinned: partial gradients add up)
+            ar.reduce(average=not args.pinned, n_buckets=args.buckets)
 
     for i in range(args.warmup):
         step(i)
@@ -257,29 +349,45 @@ def main():
     # reference's op-by-op autograd structure, vren ops + field autograd on the
     # same kernels), for the callers that keep ml_rendering.py; rank 0 at N=1.
     # Same rays and noise cycle as the headline, so the same samples per step.
-    dropin = None
+    dropin, api_step = None, None
     if args.dropin_step and world == 1:
-        from radnerf_amd.rendering import ml_render
+        from radnerf_amd.rendering import ml_render, render
 
-        def dstep(i):
+        def dstep(i, fused=False):
             model.zero_grad(set_to_none=True)
             gate.zero_grad(set_to_none=True)
-            res = ml_render(model, gate, rays_o, rays_d, rays_d, noise=noises[i % 4],
-                            exp_step_factor=esf, fused=False)
-            torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
-                                    [g_rgb, g_op, g_depth])
+            if K == 1:
+                # train.py:118 -> rendering.render (single NGP)
+                res = render(model, rays_o, rays_d, noise=noises[i % 4][0], exp_step_factor=esf,
+                             fused=fused)
+                torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
+                                        [g_rgb, g_op, g_depth[:, 0]])
+            else:
+                res = ml_render(model, gate, rays_o, rays_d, rays_d, noise=noises[i % 4],
+                                exp_step_factor=esf, fused=fused)
+                torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
+                                        [g_rgb, g_op, g_depth])
 
-        for i in range(2):
-            dstep(i)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.steps):
-            dstep(i)
-        torch.cuda.synchronize()
-        d_el = time.perf_counter() - t0
+        def timed(fused):
+            for i in range(2):
+                dstep(i, fused)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(args.steps):
+                dstep(i, fused)
+            torch.cuda.synchronize()
+            return time.perf_counter() - t0
+
+        fn = "rendering.render" if K == 1 else "rendering.ml_render"
+        d_el = timed(False)
         dropin = {"value": round(int(samples_acc) / d_el / 1e6, 2), "unit": "Msamples/s",
                   "ms_per_step": round(d_el / args.steps * 1e3, 4),
-                  "path": "rendering.ml_render (drop-in autograd chain), fwd+bwd"}
+                  "path": f"{fn}(fused=False) (drop-in op-by-op autograd chain), fwd+bwd"}
+        # the caller's own API with its default (fused) training render
+        a_el = timed(True)
+        api_step = {"value": round(int(samples_acc) / a_el / 1e6, 2), "unit": "Msamples/s",
+                    "ms_per_step": round(a_el / args.steps * 1e3, 4),
+                    "path": f"{fn}() default (fused chain through autograd), fwd+bwd"}
     # occupancy-grid maintenance (train_ml.py:174-177;
     # every 16 steps, outside the metric): the warm-up update over all
     # 128^3 x cascades cells of every sub-NeRF, and the regular update over
@@ -400,12 +508,14 @@ def main():
         rgb_linf, cpu_base = oracle_legs(args, model, gate, bits, o_np, d_np, noises[0], r,
                                          rays_o, rays_d, bg, esf, scale, seeds_np)
 
+    label = config_label(K, scale, B)
+    seen = ranks_seen(rank, local, world, None, torch.cuda.current_device())
     if args.pinned:
-        workload = (f"Rad-NeRF train_ml.py K={K} gate=ray, sub-NeRFs pinned {K // world} per GPU, "
-                    f"B={B} rays on every GPU, scale={scale}, random 128^3 occupancy "
+        workload = (f"{label} Rad-NeRF train_ml.py K={K} gate=ray, sub-NeRFs pinned {K // world} "
+                    f"per GPU, B={B} rays on every GPU, scale={scale}, random 128^3 occupancy "
                     f"p={args.occupancy:.2f}")
     else:
-        workload = (f"C3 Rad-NeRF train_ml.py K={K} gate=ray B={B}/GPU scale={scale}, "
+        workload = (f"{label} Rad-NeRF train_ml.py K={K} gate=ray B={B}/GPU scale={scale}, "
                     f"random 128^3 occupancy p={args.occupancy:.2f}")
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 2), "unit": "Msamples/s",
@@ -414,9 +524,12 @@ def main():
                "scaling": "strong" if args.pinned else "weak", "vs_baseline": None,
                "dtype": "f16/f32",
                "data": "synthetic",
+               "backend": dist.get_backend() if world > 1 else None,
+               "ranks_seen": seen,
                "config": {"workload": workload,
                           "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,
                           "occupancy": args.occupancy,
+                          "config": label,
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": f"pinned{world}" if args.pinned else f"dp{world}"},
@@ -425,6 +538,7 @@ def main():
                "forward_only": fwd_only,
                "train_step": train,
                "dropin_step": dropin,
+               "api_step": api_step,
                "density_update": density,
                "test_time_render": test_time,
                # MFMA use: algorithmic MLP flops (56,832 per sample
@@ -449,15 +563,20 @@ def _cpu_model_name():
     return None
 
 
-def _time_oracle(args_fn, reps, warm):
-    """median wall time of `reps` oracle steps after `warm` untimed ones"""
+def _time_oracle(args_fn, reps, warm, limit=None):
+    """median wall time of `reps` oracle steps after `warm` untimed ones; a
+    first step slower than `limit` s ends the timing there (an oversubscribed
+    thread count in the sweep: its one step is the figure)"""
     from oracle import ml_oracle
     ts, res = [], None
     for i in range(warm + reps):
         t0 = time.perf_counter()
         res = ml_oracle.ml_train_step(*args_fn())
+        dt = time.perf_counter() - t0
+        if i == 0 and limit is not None and dt > limit:
+            return dt, res
         if i >= warm:
-            ts.append(time.perf_counter() - t0)
+            ts.append(dt)
     return float(np.median(ts)), res
 
 
@@ -478,20 +597,45 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
     mp = model.mlp_params.detach().cpu().numpy()
     ap = gate.params.detach().cpu().numpy()
     nz = noise.cpu().numpy()
-    threads = int(os.environ.get("OMP_NUM_THREADS", 0)) or min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    from oracle import set_threads
+    nproc = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        usable = nproc
+    env_share = int(os.environ.get("OMP_NUM_THREADS", 0) or 0)
+
+    def use_threads(n):
+        torch.set_num_threads(n)
+        set_threads(n)
+
     # correctness leg: the GPU's rgb on the first n rays against the oracle's
+    use_threads(env_share or min(16, usable))
     res = ml_oracle.ml_train_step(o_np[:n], d_np[:n], bits, np.ascontiguousarray(nz[:, :n]),
                                   gp, mp, ap, scale, seeds=tuple(np.ascontiguousarray(x[:n])
                                                                  for x in seeds_np))
     rgb_linf = float(np.abs(res["rgb"] - rgb[:n]).max())
-    # (a) bounded sample of this workload
+    # (a) bounded sample of this workload, timed at each thread count: the
+    # box's CPU share (OMP_NUM_THREADS), the per-GPU share of the node
+    # (nproc / 8 GPUs) and every usable core (nproc); the
+    # baseline is the fastest
     c = args.cpu_sample_rays
     sd = tuple(np.ascontiguousarray(x[:c]) for x in seeds_np)
     nzc = np.ascontiguousarray(nz[:, :c])
-    t_a, res_a = _time_oracle(lambda: (o_np[:c], d_np[:c], bits, nzc, gp, mp, ap, scale, sd),
-                              args.cpu_reps, 3)
+    counts = sorted({t for t in (env_share, max(1, nproc // 8), usable) if t > 0})
+    sweep, best = [], None
+    for t in counts:
+        use_threads(t)
+        first = best is None
+        t_a, res_a = _time_oracle(lambda: (o_np[:c], d_np[:c], bits, nzc, gp, mp, ap, scale, sd),
+                                  args.cpu_reps if first else max(3, args.cpu_reps // 2),
+                                  3 if first else 1, None if first else 3 * best[2])
+        v = res_a["total"] / t_a / 1e6
+        sweep.append({"threads": t, "value": round(v, 5), "s_per_step": round(t_a, 3)})
+        if best is None or v > best[0]:
+            best = (v, t, t_a, res_a)
+    v_a, threads, t_a, res_a = best
+    use_threads(threads)
     # (b) C1: single NGP (K = 1), 1024 rays, scale 0.5, the same synthetic recipe
     lv = LY.grid_levels(0.5)
     g1 = S.grid_params(lv["n_entries"], seed=3).reshape(-1, 2)
@@ -502,16 +646,19 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
     s1 = S.loss_seeds(1024, 1, seed=13)
     gate1 = np.zeros(LY.gate_params(1), np.float32)        # softmax over one model = 1
     t_b, res_b = _time_oracle(lambda: (o1, d1, b1, n1, g1, m1, gate1, 0.5, s1), args.cpu_reps, 3)
-    cpu = {"value": round(res_a["total"] / t_a / 1e6, 5), "unit": "Msamples/s",
+    cpu = {"value": round(v_a, 5), "unit": "Msamples/s",
            "cores": threads, "kind": "port",
            "sample": f"{c} rays x K={args.models} ({res_a['total']} samples) of the same workload, "
                      f"fwd+bwd step of oracle/ml_oracle.py (C march/composite, OpenMP over rays; "
                      f"torch-CPU fp32 field), median of {args.cpu_reps} after 3 warm-up, "
-                     f"{t_a:.2f} s/step",
+                     f"{t_a:.2f} s/step at {threads} threads (fastest of the sweep)",
+           "thread_sweep": sweep,
            "c1": {"value": round(res_b["total"] / t_b / 1e6, 5), "unit": "Msamples/s",
+                  "threads": threads,
                   "sample": f"C1: single NGP, 1024 rays, scale 0.5 ({res_b['total']} samples), "
                             f"median of {args.cpu_reps} after 3 warm-up, {t_b:.2f} s/step"},
-           "nproc": os.cpu_count(), "cpu_model": _cpu_model_name()}
+           "nproc": nproc, "usable_cpus": usable, "omp_num_threads_env": env_share or None,
+           "cpu_model": _cpu_model_name()}
     return rgb_linf, cpu
 
 

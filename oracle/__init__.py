@@ -41,6 +41,11 @@ def lib():
     return _lib
 
 
+def set_threads(n):
+    """OpenMP threads of the C loops (bench.py's CPU-baseline thread sweep)."""
+    lib().oracle_set_threads(ctypes.c_int(int(n)))
+
+
 def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p)
 

@@ -545,3 +545,7 @@ void oracle_raymarching_train_bw(const float* dL_dxyzs, const float* dL_ddirs, c
 
 /* the compositing exponent, exported for tests/test_oracle.py's accuracy check */
 float oracle_det_expf(float x) { return det_expf(x); }
+
+/* thread count of the OpenMP loops (bench.py's CPU-baseline sweep) */
+#include <omp.h>
+void oracle_set_threads(int n) { if (n > 0) omp_set_num_threads(n); }

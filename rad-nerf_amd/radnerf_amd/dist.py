@@ -57,9 +57,12 @@ def shard_rays(n_total, rank, world):
 class GradAllReduce:
     """Flat-buffer gradient all-reduce (mean over ranks).
 
-    All gradient tensors are views of one contiguous fp32 buffer, so a step
-    issues a single large collective (45.7 MB hash-grid gradient + MLP/gate
-    gradients at scale 0.5) instead of one per parameter."""
+    All gradient tensors are views of one contiguous fp32 buffer (45.7 MB
+    hash-grid gradient + MLP/gate gradients at scale 0.5), reduced as a few
+    large asynchronous bucket collectives instead of one per parameter: a
+    few buckets keep every RCCL ring transfer large (xGMI is point-to-point,
+    ~153 GB/s per link) while the averaging / Adam of the first buckets runs
+    behind the last ones."""
 
     def __init__(self, params, device):
         self.params = list(params)
@@ -74,44 +77,72 @@ class GradAllReduce:
     def zero(self):
         self.flat.zero_()
 
-    def reduce(self, average=True):
+    def _ranges(self, n_buckets):
+        """n_buckets contiguous [a, b) ranges of the flat buffer, 64-aligned."""
+        n = self.flat.numel()
+        n_buckets = max(1, int(n_buckets))
+        bounds = sorted({min(n, (n * i // n_buckets + 63) // 64 * 64) for i in range(n_buckets)}
+                        | {n})
+        if bounds[0] != 0:
+            bounds = [0] + bounds
+        return list(zip(bounds[:-1], bounds[1:]))
+
+    def _check_views(self):
+        """Adam reads p.grad: it must still be this buffer's view, or the step
+        would use the unreduced local gradient (ranks would diverge)."""
+        for p, v in zip(self.params, self.views):
+            if p.grad is not None and p.grad.data_ptr() != v.data_ptr():
+                raise RuntimeError("GradAllReduce: a parameter's .grad was rebound away from "
+                                   "the flat gradient buffer; assign p.grad = view again")
+
+    def _launch(self, n_buckets):
+        """Asynchronous SUM all-reduce of every bucket; [(range, work)]."""
+        return [((a, b), dist.all_reduce(self.flat[a:b], async_op=True))
+                for a, b in self._ranges(n_buckets)]
+
+    def reduce(self, average=True, n_buckets=1):
+        """All-reduce the flat gradient as n_buckets asynchronous collectives;
+        each bucket's division by the world size is queued behind its own
+        work.wait() (it orders the compute stream after the collective
+        without blocking the host).  After the call the views hold the mean
+        over ranks (average) or the sum."""
         if dist.is_initialized() and dist.get_world_size() > 1:
-            dist.all_reduce(self.flat)
-            if average:
-                self.flat.div_(dist.get_world_size())
+            world = dist.get_world_size()
+            for (a, b), w in self._launch(n_buckets):
+                w.wait()
+                if average:
+                    self.flat[a:b].div_(world)
         return self.views
 
     def reduce_and_step(self, opt, n_buckets=4, average=True):
         """All-reduce + FusedAdam with the optimizer as the collective's
         epilogue: the flat gradient goes out as
-        n_buckets asynchronous all-reduces, and each bucket's Adam update is
-        queued behind its own collective (work.wait() orders the compute
-        stream after it without blocking the host), so the updates of the
-        first buckets run while the last ones are still on the wire; the mean
-        over ranks is Adam's grad_scale (no division pass).  After the call
-        the gradient views hold the rank SUM.  One rank: opt.step()."""
+        n_buckets asynchronous all-reduces, and each bucket's averaging and
+        Adam update are queued behind its own collective, so the updates of
+        the first buckets run while the last ones are still on the wire.  The
+        views are left holding what reduce() leaves (the mean over ranks with
+        average, else the sum), so code reading the gradients afterwards
+        (clipping, logging) sees the same values on either path.  One rank:
+        opt.step()."""
+        self._check_views()
         world = dist.get_world_size() if dist.is_initialized() else 1
         if world == 1:
             opt.step()
             return self.views
-        n = self.flat.numel()
-        bounds = sorted({min(n, (n * i // n_buckets + 63) // 64 * 64) for i in range(n_buckets)}
-                        | {n})
-        if bounds[0] != 0:
-            bounds = [0] + bounds
-        ranges = list(zip(bounds[:-1], bounds[1:]))
-        works = [dist.all_reduce(self.flat[a:b], async_op=True) for a, b in ranges]
+        works = self._launch(n_buckets)
         opt.begin_step()
         offs, off = [], 0
         for p in self.params:
             offs.append(off)
             off += p.numel()
-        for (a, b), w in zip(ranges, works):
+        for (a, b), w in works:
             w.wait()
+            if average:
+                self.flat[a:b].div_(world)
             for p, o in zip(self.params, offs):
                 lo, hi = max(a, o), min(b, o + p.numel())
                 if lo < hi:
-                    opt.update_range(p, lo - o, hi - o, 1.0 / world if average else 1.0)
+                    opt.update_range(p, lo - o, hi - o, 1.0)
         opt.end_step()
         return self.views
 

@@ -571,6 +571,32 @@ class _MLRenderFn(torch.autograd.Function):
         return gg, mg, ag, None, do, dd, d2, None, None, None, None
 
 
+class _GradNotSupported(torch.autograd.Function):
+    """Identity on an output the fused chain computes but does not
+    differentiate (independent_rgbs, render()'s ws): it stays on the autograd
+    graph (anchored to a parameter), and a loss that reaches it raises at
+    backward time instead of silently contributing no gradient."""
+
+    @staticmethod
+    def forward(ctx, x, anchor, what):
+        ctx.what = what
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g, _g_anchor=None):
+        raise RuntimeError(
+            f"{ctx.what}: the fused training render does not back-propagate through this "
+            "output; render with fused=False to differentiate it")
+
+
+def grad_unsupported(x, anchor, what):
+    """x as a graph output whose backward raises (see _GradNotSupported);
+    x itself (detached) when autograd is off or the anchor needs no grad."""
+    if torch.is_grad_enabled() and anchor.requires_grad:
+        return _GradNotSupported.apply(x, anchor, what)
+    return x
+
+
 _RENDERERS = collections.OrderedDict()
 MAX_RENDERERS = 4       # workspaces are ~0.3 GB per 1k rays x sub-NeRF: keep a few
 
@@ -617,6 +643,10 @@ def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **k
         model.xyz_encoder.params, model.mlp_params, gating_net.params, r, rays_o, rays_d, second,
         noise.contiguous(), bg, float(kwargs.get("T_threshold", 1e-4)), esf)
     w = r.ws
-    singles = [(w.rgb_k[i] + bg * (1 - w.opacity_k[i])[:, None]).detach() for i in range(K)]
+    # each sub-NeRF's own colour (ml_rendering.py:65,73): values only -- a loss
+    # on them raises at backward (the fused backward seeds the combined rgb)
+    singles = [grad_unsupported(w.rgb_k[i] + bg * (1 - w.opacity_k[i])[:, None],
+                                model.mlp_params, "ml_render independent_rgbs")
+               for i in range(K)]
     return {"rgb": rgb, "independent_rgbs": singles, "depth": depth, "opacity": opacity,
             "gating_code": gate, "gating_importance": gate.sum(0)}

@@ -489,8 +489,9 @@ class NGP(MNGP):
 
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False,
-                            generator=None):
-        super().update_density_grid(density_threshold, warmup, decay, erode, generator)
+                            generator=None, seed=None):
+        return super().update_density_grid(density_threshold, warmup, decay, erode, generator,
+                                           seed)
 
 
 class _GateFn(torch.autograd.Function):

@@ -24,6 +24,7 @@ import torch
 from . import vren
 from ._lib import lib
 from .custom_functions import RayAABBIntersector, RayMarcher, VolumeRenderer
+from .fused import grad_unsupported
 
 MAX_SAMPLES = 1024
 NEAR_DISTANCE = 0.01
@@ -139,9 +140,90 @@ def _test_fused(model, rays_o, rays_d, hits_t, kw):
              "total_samples": n_smp[i].sum(), "deltas": None} for i in range(K)]
 
 
+class _SingleGate:
+    """Gate of a single NGP for the fused renderer: softmax over one model is
+    exactly 1, so the renderer skips the gate MLP (no parameters)."""
+    out_dim = 1
+    type = "ray"
+
+    def __init__(self, device):
+        self.params = torch.zeros(0, device=device)
+
+
+def _single_gate(model):
+    g = getattr(model, "_fused_single_gate", None)
+    if g is None or g.params.device != model.mlp_params.device:
+        g = _SingleGate(model.mlp_params.device)
+        model._fused_single_gate = g
+    return g
+
+
+class _TrainResults(dict):
+    """render()'s training result on the fused chain.  rgb / opacity / depth
+    are there at once; the per-sample keys of __render_rays_train
+    (rendering.py:207-239: rays_a, ws, deltas, ts, rm_samples, vr_samples) are
+    copied out of the renderer's workspace on first access (one read-back of
+    the sample count), so a training step that only reads rgb / opacity pays
+    nothing for them.  Reading them after another forward has reused the
+    workspace raises.  ws carries no gradient through the fused chain: a
+    loss on it (e.g. a distortion loss) raises at backward."""
+    LAZY = ("rays_a", "ws", "deltas", "ts", "rm_samples", "vr_samples")
+
+    def __init__(self, base, renderer, anchor):
+        super().__init__(base)
+        self._r, self._gen, self._anchor = renderer, renderer.ws.generation, anchor
+
+    def __contains__(self, key):
+        return super().__contains__(key) or key in self.LAZY
+
+    def __missing__(self, key):
+        if key not in self.LAZY:
+            raise KeyError(key)
+        w = self._r.ws
+        if w.generation != self._gen:
+            raise RuntimeError(f"render(): '{key}' read after another forward reused the "
+                               "renderer's workspace; read it before the next render")
+        n = int(w.meta[1])                      # K = 1: segment 0 starts at 0
+        if key == "rays_a":
+            v = torch.stack((torch.arange(w.B, device=w.device, dtype=torch.int32),
+                             w.offsets[0], w.counts[0]), 1)
+        elif key == "ws":
+            v = grad_unsupported(w.ws[:n], self._anchor, "render() ws")
+        elif key == "deltas":
+            v = w.deltas[:n].clone()
+        elif key == "ts":
+            v = w.ts[:n].clone()
+        elif key == "rm_samples":
+            v = w.meta[1].clone()
+        else:
+            v = w.used.sum()
+        self[key] = v
+        return v
+
+
+def _train_fused(model, rays_o, rays_d, kw):
+    """rendering.py:192-239 on the fused K = 1 chain (radnerf_amd.fused):
+    march, field, composite and background as one launch chain forward and
+    backward, merged fixed-point grid-gradient scatter, no host sync."""
+    from .fused import get_renderer, ml_render_fused
+    gate = _single_gate(model)
+    kw = dict(kw)
+    noise = kw.pop("noise", None)
+    if noise is not None:
+        kw["noise"] = noise.reshape(1, -1)
+    res = ml_render_fused(model, gate, rays_o, rays_d, rays_d, **kw)
+    r = get_renderer(model, gate, rays_o.shape[0], grad=torch.is_grad_enabled())
+    return _TrainResults({"rgb": res["rgb"], "opacity": res["opacity"],
+                          "depth": res["depth"][:, 0]}, r, model.mlp_params)
+
+
 def render(model, rays_o, rays_d, **kwargs):
-    """rendering.py:12-46 for a single NGP model."""
+    """rendering.py:12-46 for a single NGP model.  Training renders take the
+    fused chain (fused=True, the default); fused=False keeps the reference's
+    op-by-op autograd structure (RayMarcher -> model -> VolumeRenderer)."""
     fused = kwargs.pop("fused", True)
+    if fused and not kwargs.get("test_time", False):
+        return _to_host(_train_fused(model, rays_o, rays_d, kwargs), kwargs)
     with torch.autocast("cuda"):
         rays_o, rays_d = rays_o.contiguous(), rays_d.contiguous()
         hits_t = _near_far(model, rays_o, rays_d)
@@ -176,7 +258,7 @@ def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs)
         rgb_acc = torch.zeros(B, 3, device=dev)
         op_acc = torch.zeros(B, device=dev)
         depth_all = torch.zeros(B, K, device=dev)
-        singles = []
+        singles, total_k = [], []
         noise = kwargs.pop("noise", None)
         fn = _test_rays if kwargs.get("test_time", False) else _train_rays
         test_fused = None
@@ -198,8 +280,13 @@ def ml_render(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs)
                        call, kw)
                 r = _to_host(r, kwargs)
             singles.append(r["rgb"])
+            total_k.append(r["total_samples"] if "total_samples" in r else 0)
             rgb_acc = rgb_acc + r["rgb"] * gate[:, i][:, None]
             depth_all[:, i] = r["depth"]
             op_acc = op_acc + r["opacity"] * gate[:, i]
-        return {"rgb": rgb_acc, "independent_rgbs": singles, "depth": depth_all,
-                "opacity": op_acc, "gating_code": gate, "gating_importance": importance}
+        out = {"rgb": rgb_acc, "independent_rgbs": singles, "depth": depth_all,
+               "opacity": op_acc, "gating_code": gate, "gating_importance": importance}
+        if kwargs.get("test_time", False):
+            # samples composited over all sub-NeRFs (a device scalar)
+            out["total_samples"] = sum(total_k)
+        return out

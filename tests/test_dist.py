@@ -55,6 +55,13 @@ def _worker(rank, world, port, q):
         views = ar.reduce()
         ok_mean = all(torch.allclose(v, torch.full_like(v, 1.5 * (i + 1)))
                       for i, v in enumerate(views))
+        # the same as 3 asynchronous buckets (bench.py's headline N>1 step)
+        for i, v in enumerate(ar.views):
+            v.copy_(torch.arange(v.numel(), dtype=torch.float32).view_as(v) * (rank + 1) + i)
+        views = ar.reduce(n_buckets=3)
+        ok_mean = ok_mean and all(
+            torch.allclose(v, (torch.arange(v.numel(), dtype=torch.float32).view_as(v) * 1.5 + i))
+            for i, v in enumerate(views))
         # density buffers synchronised from rank 0
         m = torch.nn.Module()
         m.register_buffer("density_bitfield_0", torch.full((8,), rank, dtype=torch.uint8))
@@ -70,7 +77,7 @@ def _worker(rank, world, port, q):
         dist.all_gather(got, draw)
         ok_stream = all(torch.equal(x, draw) for x in got) and not torch.equal(draw, other)
         # bucketed all-reduce with the optimizer as its epilogue: every element
-        # updated exactly once, from its bucket's summed gradient, at scale 1/world
+        # updated exactly once, from its bucket's averaged gradient (scale 1)
         params2 = [torch.zeros(1000), torch.zeros(37), torch.zeros(5)]
         ar2 = rdist.GradAllReduce(params2, "cpu")
         for p_, v in zip(params2, ar2.views):
@@ -85,10 +92,20 @@ def _worker(rank, world, port, q):
             for q_, lo_, hi_, sc in opt.calls:
                 if q_ is p_:
                     seen[lo_:hi_] += 1
-                    ok_epi = ok_epi and sc == 1.0 / world
-                    # the bucket's sum had landed when its update was queued
+                    ok_epi = ok_epi and sc == 1.0
+                    # the bucket's mean had landed when its update was queued
                     ok_epi = ok_epi and torch.equal(opt.snap[(id(q_), lo_)], v[lo_:hi_])
             ok_epi = ok_epi and bool((seen == 1).all())
+        # the views hold the mean, as after reduce()
+        for i, v in enumerate(ar2.views):
+            ok_epi = ok_epi and torch.equal(v, torch.arange(v.numel(), dtype=torch.float32) * 1.5 + i)
+        # a .grad rebound away from the flat buffer is refused
+        params2[1].grad = torch.zeros(37)
+        try:
+            ar2.reduce_and_step(opt)
+            ok_epi = False
+        except RuntimeError:
+            pass
         q.put((rank, lo, hi, ok_mean, ok_bcast and ok_stream and ok_epi))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -116,3 +133,39 @@ def test_single_process_noop():
     assert torch.equal(ar.reduce()[0], torch.full((3,), 2.0))
     assert rdist.shard_rays(10, 0, 1) == (0, 10)
     assert rdist.shard_rays(10, 2, 3) == (8, 10)
+
+
+def test_bench_self_launch_gloo():
+    """bench.py --gpus 2 with no torchrun environment starts 2 ranks itself
+    (torch.distributed.run child process), checks the world size and reports
+    the ranks it saw (--launch-check: no GPU work, gloo on CPU)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                          "--backend", "gloo", "--launch-check"], env=env, capture_output=True,
+                         text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1]
+    rec = json.loads(line)
+    assert rec["n_gpus"] == 2 and rec["backend"] == "gloo"
+    assert sorted(r["rank"] for r in rec["ranks_seen"]) == [0, 1]
+
+
+def test_bench_world_mismatch_fails():
+    """A torchrun world that differs from --gpus exits non-zero."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                          "--nproc-per-node=2", "--master-addr=127.0.0.1",
+                          f"--master-port={_free_port()}", os.path.join(root, "bench.py"),
+                          "--gpus", "4", "--backend", "gloo", "--launch-check"],
+                         env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode != 0
+    assert "--gpus 4 but the process group has 2" in out.stderr

@@ -73,11 +73,10 @@ def test_data_parallel_training_stays_identical(tmp_path):
 
 def test_bucketed_adam_epilogue_matches_plain(tmp_path):
     """GradAllReduce.reduce_and_step (4 asynchronous all-reduce buckets, each
-    bucket's FusedAdam update queued behind its collective, the 1/world mean
-    as Adam's grad_scale) vs reduce() (one collective + division) +
-    FusedAdam.step(), on identical per-rank gradients, 3 steps, buckets cutting
-    across parameters: bit-identical parameters and moments on both ranks
-    (world = 2: the division by 2 and the scale by 1/2 are both exact)."""
+    bucket's division by the world size and FusedAdam update queued behind its
+    collective) vs reduce() (one collective + division) + FusedAdam.step(),
+    on identical per-rank gradients, 3 steps, buckets cutting across
+    parameters: bit-identical parameters and moments on both ranks."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     res = _run_ranks("adam_worker.py", tmp_path / "adam.json", timeout=100)

@@ -2,8 +2,10 @@
 
 Bars (BASELINE.json north_star):
   * ray/AABB, march counts, sample t/dt/xyz, Morton, packbits: bit-exact;
-  * composite rgb/depth/opacity: |diff| <= 1e-4 (fp32; the kernel uses the
-    wave prefix-product + __expf, the oracle a serial loop with expf);
+  * composite rgb/depth/opacity: |diff| <= 1e-4 (fp32; the kernel folds T as
+    a wave prefix product, the oracle serially; both evaluate exp(-sigma*dt)
+    with the same deterministic sequence, rn_exp_det / det_expf), and the
+    termination (which samples get weights) bit-exact;
   * field (f16 MFMA, fp32 accumulate) vs the torch fp32 oracle with the same
     f16 rounding points: tolerances stated per test.
 """

@@ -40,7 +40,12 @@ def _init(m, K, p=0.5):
     return bits
 
 
-def test_ngp_render_train_vs_oracle(cuda):
+@pytest.mark.parametrize("fused", [True, False])
+def test_ngp_render_train_vs_oracle(cuda, fused):
+    """a11: render() training render of a single NGP, fused K = 1 chain (the
+    default) and the op-by-op chain, vs the oracle: counts bit-exact, outputs
+    <= 1e-4, per-level / per-layer gradient bars; the per-sample keys
+    (rays_a, ts, deltas, ws, rm_samples, vr_samples) vs the oracle too."""
     scale, B = 0.5, 512
     m = NGP(scale, seed=3)
     bits = _init(m, 1)
@@ -49,15 +54,29 @@ def test_ngp_render_train_vs_oracle(cuda):
     nz = S.noise(1, B)
     d_rgb, d_op, d_depth = S.loss_seeds(B, 1)
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
-    res = render(m, t(o), t(d), noise=t(nz[0]))
+    res = render(m, t(o), t(d), noise=t(nz[0]), fused=fused)
     torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
                             [t(d_rgb), t(d_op), t(d_depth[:, 0])])
+    for k in ("rays_a", "ws", "deltas", "ts", "rm_samples", "vr_samples"):
+        assert k in res
+    n = int(res["rm_samples"])
+    ra = res["rays_a"].cpu().numpy()
+    assert ra.shape == (B, 3) and int(ra[:, 2].sum()) == n
+    assert res["ts"].shape == (n,) and res["deltas"].shape == (n,) and res["ws"].shape == (n,)
+    # per-ray segments: contiguous, in ray order, the weights of a ray sum to
+    # its opacity
+    assert np.array_equal(ra[:, 0], np.arange(B))
+    ws_np = res["ws"].detach().cpu().numpy()
+    op_np = res["opacity"].detach().cpu().numpy()
+    seg = np.add.reduceat(ws_np, ra[:, 1]) if n else np.zeros(B)
+    has = ra[:, 2] > 0
+    assert np.allclose(seg[has], op_np[has], atol=1e-5)
+    assert 0 < int(res["vr_samples"]) <= n
     gate_p = np.zeros(LY.gate_params(1), np.float32)    # softmax over one model = 1
     ref = ml_oracle.ml_train_step(o, d, bits, nz, m.xyz_encoder.params.detach().cpu().view(-1, 2),
                                   m.mlp_params.detach().cpu(), gate_p, scale,
                                   seeds=(d_rgb, d_op, d_depth))
     # bit-exact sample counts per ray
-    ra = res["rays_a"].cpu().numpy()
     assert np.array_equal(ra[:, 2], ref["counts"][0])
     e_rgb = np.abs(res["rgb"].detach().cpu().numpy() - ref["rgb"]).max()
     e_op = np.abs(res["opacity"].detach().cpu().numpy() - ref["opacity"]).max()
@@ -254,3 +273,90 @@ def test_density_update_sampled_device(cuda, scale, K):
         assert abs(thr_dev[k] - min(mean, thr)) <= 1e-5 * min(mean, thr), (thr_dev[k], mean)
         bits = oracle.packbits(new.cpu().numpy().reshape(-1), float(thr_dev[k]))
         assert np.array_equal(getattr(m, f"density_bitfield_{k}").cpu().numpy(), bits)
+
+
+def _ngp_setup(cuda, B, scale=0.5, p=0.5):
+    m = NGP(scale, seed=3)
+    bits = _init(m, 1, p=p)
+    m = m.to(cuda)
+    o, d = S.rays(B, scale)
+    return m, bits, o, d
+
+
+def test_ngp_render_fused_full_size(cuda):
+    """render() at C2's batch (8192 rays): the fused K = 1 chain vs the
+    op-by-op chain on the same jitter -- outputs <= 1e-5, per-sample keys
+    bit-identical (same march), gradients <= 1e-3 rel; count conservation."""
+    B = 8192
+    m, _, o, d = _ngp_setup(cuda, B)
+    nz = torch.from_numpy(S.noise(1, B)[0]).to(cuda)
+    seeds = [torch.from_numpy(np.ascontiguousarray(s)).to(cuda) for s in S.loss_seeds(B, 1)]
+    outs = []
+    for fused in (True, False):
+        m.zero_grad()
+        res = render(m, torch.from_numpy(o).to(cuda), torch.from_numpy(d).to(cuda), noise=nz,
+                     fused=fused)
+        torch.autograd.backward([res["rgb"], res["opacity"], res["depth"]],
+                                [seeds[0], seeds[1], seeds[2][:, 0]])
+        keys = {k: res[k].detach().clone() for k in ("rays_a", "ts", "deltas", "ws", "rm_samples")}
+        outs.append((res, keys, m.xyz_encoder.params.grad.clone(), m.mlp_params.grad.clone()))
+    (rf, kf, gf, mf), (rd, kd, gd, md) = outs
+    for k in ("rgb", "opacity", "depth"):
+        assert (rf[k].detach() - rd[k].detach()).abs().max().item() <= 1e-5, k
+    for k in ("rays_a", "ts", "deltas", "rm_samples"):
+        assert torch.equal(kf[k], kd[k]), k
+    assert (kf["ws"] - kd["ws"]).abs().max().item() <= 1e-5
+    assert int(kf["rays_a"][:, 2].sum()) == int(kf["rm_samples"]) > 0
+    for a, b in ((gf, gd), (mf, md)):
+        e = ((a - b).norm() / b.norm()).item()
+        assert e <= 1e-3, e
+
+
+def test_ngp_render_test_time_vs_oracle(cuda):
+    """a10 + a11: render(test_time=True) of a single NGP (rn_render_test, and
+    the host loop with fused=False) vs the oracle's compaction loop (K = 1)."""
+    B, scale = 600, 0.5
+    m, bits, o, d = _ngp_setup(cuda, B, p=0.3)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    with torch.no_grad():
+        te = render(m, t(o), t(d), test_time=True)
+        lp = render(m, t(o), t(d), test_time=True, fused=False)
+    gate_p = np.zeros(LY.gate_params(1), np.float32)
+    ref = ml_oracle.ml_render_test(o, d, bits, m.xyz_encoder.params.detach().cpu().view(-1, 2),
+                                   m.mlp_params.detach().cpu(), gate_p, scale)
+    for name, res in (("fused", te), ("loop", lp)):
+        errs = {"rgb": float(np.abs(res["rgb"].float().cpu().numpy() - ref["rgb"]).max()),
+                "opacity": float(np.abs(res["opacity"].float().cpu().numpy() - ref["opacity"]).max()),
+                "depth": float(np.abs(res["depth"].float().cpu().numpy().reshape(-1)
+                                      - np.asarray(ref["depth"]).reshape(-1)).max())}
+        assert all(v <= 1e-4 for v in errs.values()), (name, errs)
+    assert int(te["total_samples"]) > 0
+
+
+def test_fused_outputs_without_gradient_raise(cuda):
+    """independent_rgbs (ml_render) and ws (render) come out of the fused
+    chain as values; a loss on them raises at backward instead of silently
+    getting no gradient (fused=False differentiates them)."""
+    from radnerf_amd.fused import ml_render_fused
+    from tests_parity_helpers import setup_ml
+    B, K = 256, 2
+    m, g, o, d, noise, seeds, bits = setup_ml(cuda, B, K, 0.5)
+    to = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+    res = ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
+    assert res["independent_rgbs"][0].requires_grad
+    with pytest.raises(RuntimeError, match="independent_rgbs"):
+        res["independent_rgbs"][1].sum().backward()
+    # the combined outputs still differentiate
+    res = ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
+    res["rgb"].sum().backward()
+    assert m.mlp_params.grad is not None
+    # render()'s ws
+    mn, _, on, dn = _ngp_setup(cuda, B)
+    r1 = render(mn, to(on), to(dn))
+    with pytest.raises(RuntimeError, match="ws"):
+        r1["ws"].sum().backward()
+    # a second forward through the same workspace makes the lazy keys stale
+    r2 = render(mn, to(on), to(dn))
+    with pytest.raises(RuntimeError, match="reused"):
+        _ = r1["ts"]
+    assert r2["ts"].numel() == int(r2["rm_samples"])
