@@ -114,6 +114,10 @@ def parse():
     ap.add_argument("--pinned", action="store_true",
                     help="sub-NeRF-per-GPU layout (SURVEY.md §8(e) C5): rank r renders ALL rays "
                          "for its K/N sub-NeRFs, per-ray outputs all-gathered (strong scaling)")
+    ap.add_argument("--pinned-sim", type=int, default=0,
+                    help="one GPU: time rank 0's share of the pinned layout over this many "
+                         "ranks (its K/P sub-NeRFs over all rays + the gate backward; the "
+                         "all-gather replaced by local copies, no collectives)")
     ap.add_argument("--backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="process-group backend (auto: RCCL on GPUs); gloo only to rehearse the "
                          "multi-rank path on one GPU")
@@ -212,7 +216,7 @@ def main():
         for i in range(K):
             getattr(model, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
     # data parallel: every rank its own rays; pinned: the same rays on every rank
-    rs = 0 if args.pinned else rank
+    rs = 0 if (args.pinned or args.pinned_sim) else rank
     o_np, d_np = S.rays(B, scale, seed=1000 * rs)
     rays_o = torch.from_numpy(o_np).to(dev)
     rays_d = torch.from_numpy(d_np).to(dev)
@@ -221,7 +225,12 @@ def main():
     g_rgb, g_op, g_depth = (torch.from_numpy(s).to(dev) for s in seeds_np)
     bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
 
-    if args.pinned:
+    if args.pinned_sim:
+        if world != 1:
+            raise SystemExit("--pinned-sim runs on one process")
+        from radnerf_amd.pinned import PinnedMLRenderer
+        r = PinnedMLRenderer(model, gate, B, sim=(0, args.pinned_sim))
+    elif args.pinned:
         from radnerf_amd.pinned import PinnedMLRenderer
         r = PinnedMLRenderer(model, gate, B)
     else:
@@ -244,6 +253,7 @@ def main():
             # own wait (pinned: partial gradients add up)
             ar.reduce(average=not args.pinned, n_buckets=args.buckets)
 
+    log(f"rank {rank}/{world}: warm-up ({args.warmup} steps)")
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
@@ -311,6 +321,7 @@ def main():
     # (all-reduce) -> FusedAdam; synthetic target colours.  Not part of `value`.
     train = None
     if args.train_step:
+        log("train step leg")
         from radnerf_amd.optim import FusedAdam
         params = [model.xyz_encoder.params, model.mlp_params, gate.params]
         for p_, v_ in zip(params, ar.views):
@@ -351,6 +362,7 @@ def main():
     # Same rays and noise cycle as the headline, so the same samples per step.
     dropin, api_step = None, None
     if args.dropin_step and world == 1:
+        log("drop-in / API legs")
         from radnerf_amd.rendering import ml_render, render
 
         def dstep(i, fused=False):
@@ -394,6 +406,7 @@ def main():
     # 128^3/4 uniform + 128^3/4 occupied cells, rank-consistent stream
     density = None
     if args.density_update:
+        log("density-update leg")
         thr = 0.01 * 1024 / 3 ** 0.5
         dms = {}
         # the update rewrites the occupancy buffers: restore them afterwards
@@ -418,6 +431,7 @@ def main():
     # --test-time-rays rays through ml_render(test_time=True); not part of `value`
     test_time = None
     if args.test_time_rays and world == 1:
+        log("test-time render leg")
         from radnerf_amd.rendering import ml_render
         nt = args.test_time_rays
         ot, dt_ = (torch.from_numpy(a).to(dev) for a in S.rays(nt, scale, seed=99))
@@ -505,12 +519,18 @@ def main():
     rgb_linf = None
     cpu_base = None
     if rank == 0 and world == 1 and args.cpu_rays > 0:
+        log("oracle legs (rgb check, CPU baseline)")
         rgb_linf, cpu_base = oracle_legs(args, model, gate, bits, o_np, d_np, noises[0], r,
                                          rays_o, rays_d, bg, esf, scale, seeds_np)
 
-    label = config_label(K, scale, B)
+    label = config_label(K, scale, B if not (args.pinned or args.pinned_sim) else 8192)
     seen = ranks_seen(rank, local, world, None, torch.cuda.current_device())
-    if args.pinned:
+    if args.pinned_sim:
+        workload = (f"{label} Rad-NeRF train_ml.py K={K} gate=ray, pinned layout simulated on one "
+                    f"GPU: rank 0 of {args.pinned_sim} ({K // args.pinned_sim} sub-NeRF(s) over "
+                    f"all B={B} rays + gate backward; all-gather by local copies, no all-reduce), "
+                    f"scale={scale}, random 128^3 occupancy p={args.occupancy:.2f}")
+    elif args.pinned:
         workload = (f"{label} Rad-NeRF train_ml.py K={K} gate=ray, sub-NeRFs pinned {K // world} "
                     f"per GPU, B={B} rays on every GPU, scale={scale}, random 128^3 occupancy "
                     f"p={args.occupancy:.2f}")
@@ -532,7 +552,8 @@ def main():
                           "config": label,
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
-                          "parallelism": f"pinned{world}" if args.pinned else f"dp{world}"},
+                          "parallelism": (f"pinned{args.pinned_sim}-rank0-sim" if args.pinned_sim
+                                          else f"pinned{world}" if args.pinned else f"dp{world}")},
                "roofline": roofline, "cpu_baseline": cpu_base,
                "rgb_linf_vs_ref": rgb_linf,
                "forward_only": fwd_only,
@@ -550,6 +571,34 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def log(msg):
+    """progress on stderr (a long leg must not look hung to the GPU-box watchdog)"""
+    sys.stderr.write(f"[bench {time.strftime('%H:%M:%S')}] {msg}\n")
+    sys.stderr.flush()
+
+
+def _cgroup_cpus():
+    """CPUs the cgroup quota allows (cpu.max), or None when unlimited/unknown."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            if q != "max":
+                return max(1, int(int(q) / int(per)))
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
 
 
 def _cpu_model_name():
@@ -573,6 +622,7 @@ def _time_oracle(args_fn, reps, warm, limit=None):
         t0 = time.perf_counter()
         res = ml_oracle.ml_train_step(*args_fn())
         dt = time.perf_counter() - t0
+        log(f"  oracle step {i + 1}/{warm + reps}: {dt:.2f} s")
         if i == 0 and limit is not None and dt > limit:
             return dt, res
         if i >= warm:
@@ -604,6 +654,7 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
     except (AttributeError, OSError):
         usable = nproc
     env_share = int(os.environ.get("OMP_NUM_THREADS", 0) or 0)
+    quota = _cgroup_cpus()
 
     def use_threads(n):
         torch.set_num_threads(n)
@@ -622,9 +673,15 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
     c = args.cpu_sample_rays
     sd = tuple(np.ascontiguousarray(x[:c]) for x in seeds_np)
     nzc = np.ascontiguousarray(nz[:, :c])
-    counts = sorted({t for t in (env_share, max(1, nproc // 8), usable) if t > 0})
+    counts = sorted({t for t in (env_share, max(1, nproc // 8), nproc, usable) if t > 0})
     sweep, best = [], None
     for t in counts:
+        if quota is not None and t > quota and best is not None:
+            # more threads than the cgroup's CPU quota lets run: not a
+            # measurement of t cores (recorded as skipped)
+            sweep.append({"threads": t, "skipped": f"cgroup CPU quota {quota} CPUs"})
+            continue
+        log(f"cpu baseline: {t} threads")
         use_threads(t)
         first = best is None
         t_a, res_a = _time_oracle(lambda: (o_np[:c], d_np[:c], bits, nzc, gp, mp, ap, scale, sd),
@@ -657,7 +714,8 @@ def oracle_legs(args, model, gate, bits, o_np, d_np, noise, r, rays_o, rays_d, b
                   "threads": threads,
                   "sample": f"C1: single NGP, 1024 rays, scale 0.5 ({res_b['total']} samples), "
                             f"median of {args.cpu_reps} after 3 warm-up, {t_b:.2f} s/step"},
-           "nproc": nproc, "usable_cpus": usable, "omp_num_threads_env": env_share or None,
+           "nproc": nproc, "usable_cpus": usable, "cgroup_cpu_quota": quota,
+           "omp_num_threads_env": env_share or None,
            "cpu_model": _cpu_model_name()}
     return rgb_linf, cpu
 

@@ -231,15 +231,20 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
 /* Fixed-point accumulation of the hashed levels' grid gradient (fx_mode 2,
  * the fused renderer's default; needs the encoding cache).  fx_acc: int32, one
  * per grid_grad element, zero on entry; fx_scale [16] f32 per level: 2^e_l, or
- * 0 for fp32 atomics into grid_grad (dense levels, first step); fx_vmax [16]
- * u32: the kernel atomic-maxes the bits of each level's largest |record|.
+ * 0 for fp32 atomics into grid_grad (dense levels, first step); fx_vmax: the
+ * 384-B per-level statistics block, zero before the first step: u32 vmax[16]
+ * (the kernel atomic-maxes the bits of each level's largest |record|),
+ * u32 pad[16], f64 qsum[16] (the sum of each level's integer records),
+ * i64 esum[16] (rn_grid_fx_fold: the exact sum of the level's int32 entries).
  * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
  * memory side serves them ~27 % faster than f32 adds), so those levels'
  * gradients are order-independent and bitwise reproducible.
  * rn_grid_fx_fold then (1) sets *fx_redo when a level's largest record reached
- * 2^22 units or was not finite, writes the next step's scales
+ * 2^22 units or was not finite, or when the level's entry sum differs from its
+ * record sum by more than 2^31 (an int32 entry wrapped: many same-sign
+ * records), writes the next step's scales
  * (2^(19 - e), |record| < 2^e; dense levels 0) to fx_scale_next and clears
- * fx_vmax, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
+ * the statistics, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
  * and re-zeroes fx_acc.  The caller then launches rn_field_bwd_merged with
  * fx_mode 3 and the same fx_scale (fp32 redo of the fixed-point levels' grid
  * scatter, no dW): it returns at once unless *fx_redo is set; and swaps
@@ -350,14 +355,17 @@ int rn_field_dinput(const float* xyzs, const float* dirs, int64_t n_samples, con
  * sub-NeRFs and cascades in one call, no host synchronisation.  grid_ptrs /
  * bitfield_ptrs: device arrays of n_models pointers to the (cascades, 128^3)
  * f32 density grids (updated in place) and their bitfields.  Per (sub-NeRF,
- * cascade): 128^3/4 uniform cells and 128^3/4 cells drawn among those with
- * density > threshold, jittered in the cell, drawn from a counter-based hash
- * of `seed` (same seed -> same cells on every rank); sigma from the grid + geo
+ * cascade): the draws of 128^3/4 uniform cells and 128^3/4 cells among those
+ * with density > threshold, as per-cell Poisson counts (rates 1/4 and
+ * (128^3/4) / n_occupied, at most 31 per cell) from a counter-based hash of
+ * `seed` (same seed -> same draws on every rank), listed and evaluated in cell
+ * (Morton) order; each draw jittered in its cell; sigma from the grid + geo
  * MLP (frags: [n_models][46 * 512] f16); duplicates keep their max; then
  * grid = grid < 0 ? grid : max(grid * decay, sampled), packbits at
  * min(mean of the positive cells, threshold) (thr_out [n_models]).
- * Scratch: tmp, occ (n_models * cascades * 128^3 f32 / i32), blk
- * (n_models * cascades * 128^3 / 1024 + 1 i32), part (n_models * 1024 f32).   */
+ * Scratch: tmp, occ (the draw list) (n_models * cascades * 128^3 f32 / i32),
+ * blk (2 * (n_models * cascades * 128^3 / 1024 + 1) i32), part
+ * (n_models * 1024 f32).  cascades <= 32.                                     */
 int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, int32_t n_models,
                               int32_t cascades, int32_t grid_size, float scale,
                               float density_threshold, float decay, uint64_t seed,

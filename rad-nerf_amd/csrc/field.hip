@@ -290,12 +290,16 @@ struct Walk2 {
     // the largest |record| issued for each, as float bits (NaN/inf included)
     float fxA, fxB;
     uint32_t vmA, vmB;
+    // ... and the sum of the integer records issued for each (float: the
+    // net-wrap check of rn_grid_fx_fold needs it to well within 2^31)
+    float sqA, sqB;
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     W.ring = ring; W.head = 0; W.tail = 0; W.pend = 0;
     W.ex0 = W2_NONE; W.ex1 = W2_NONE; W.ey = 0; W.ez = 0; W.cur0 = 0; W.cur1 = 0;
     W.a00 = W.a01 = W.a10 = W.a11 = 0.f;
+    W.sqA = W.sqB = 0.f;
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
     W.offA = W.offB = 0;
 }
@@ -337,10 +341,23 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // the fixed-point sums and the GM 3 launch redoes the grid scatter in fp32.
 // Dense levels (few requests: merged per ray) and the first step (scale 0)
 // use fp32 atomics.
+// An int32 entry can still wrap with every record under 2^22 units (many
+// same-sign records on one entry); the kernel therefore also sums each
+// level's integer records (per lane in float, per wave in double), and
+// rn_grid_fx_fold sums the level's int32 entries exactly: a wrapped entry
+// makes the two differ by a multiple of 2^32, which sets the redo flag too.
+struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats block
+    uint32_t vmax[RN_L];   // largest |record| this step (float bits, atomicMax)
+    uint32_t pad[RN_L];
+    double qsum[RN_L];     // sum of the issued integer records
+    int64_t esum[RN_L];    // sum of the int32 entries (rn_grid_fx_fold)
+};
+
 struct FxGrad {
     int32_t* acc;              // int32 [entries][2]
     const float* scale;        // [RN_L] 2^e_l, 0 = fp32 atomics for the level
-    uint32_t* vmax;            // [RN_L] largest |record| this step (float bits, atomicMax)
+    uint32_t* vmax;            // FxStats::vmax
+    double* qsum;              // FxStats::qsum
     const int32_t* redo;       // GM 3: the launch runs only when *redo != 0
     __amdgpu_buffer_rsrc_t rs; // over acc (built in the kernel)
 };
@@ -393,6 +410,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             int q;
             asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
+            if (odd) W.sqB += (float)q; else W.sqA += (float)q;
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -965,6 +983,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     // fixed point: this wave's two levels' scales (wave-uniform) and maxima
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
+    float sqA = 0.f, sqB = 0.f;
     if (GM >= 2) {
         fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
         fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
@@ -1081,7 +1100,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         const int elen_lane = max(0, min(E, n_p - (rn_lane() >> 3) * E));   // walk eighth
         Walk2 W;
         walk2_begin(W, ring2);
-        W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB;
+        W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB; W.sqA = sqA; W.sqB = sqB;
         for (int w0 = 0; w0 < E; w0 += 32) {
             const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
             const int e = j >> 5, jj = j & 31;
@@ -1122,15 +1141,23 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
             __syncthreads();
         }
         walk2_end<GM>(a, sT, grad_rs, G, W, dbg);
-        vmA = W.vmA; vmB = W.vmB;
+        vmA = W.vmA; vmB = W.vmB; sqA = W.sqA; sqB = W.sqB;
         __syncthreads();                         // rings (image region) drained
     }
     if (GM == 2) {                               // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
         vmB = rn_wave_max_u32(vmB);
+        double dA = (double)sqA, dB = (double)sqB;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            dA += __shfl_xor(dA, off);
+            dB += __shfl_xor(dB, off);
+        }
         if (rn_lane() == 0) {
             if (vmA) atomicMax(F.vmax + wid, vmA);
             if (vmB) atomicMax(F.vmax + RN_L - 1 - wid, vmB);
+            if (dA != 0.0) atomicAdd(F.qsum + wid, dA);
+            if (dB != 0.0) atomicAdd(F.qsum + RN_L - 1 - wid, dB);
         }
     }
     // ---- flush every model's dW (the current one from registers)
@@ -1320,22 +1347,52 @@ k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
 // scale (8x growth since the step the scale came from), or a non-finite one,
 // sets the redo flag: rn_grid_fx_fold then discards the fixed-point sums and
 // the GM 3 launch recomputes the grid gradient in fp32.
+// Exact per-level sum of the int32 entries (int64), for the net-wrap check.
+__global__ void __launch_bounds__(256)
+k_fx_esum(GridMeta gm, uint32_t hashed_mask, const int32_t* __restrict__ acc,
+          FxStats* __restrict__ st) {
+    const int l = blockIdx.y;
+    if (!((hashed_mask >> l) & 1u)) return;
+    typedef int vi4 __attribute__((ext_vector_type(4)));
+    const int64_t e0 = 2 * (int64_t)gm.offset[l], n4 = (2 * (int64_t)gm.hsize[l]) >> 2;
+    const vi4* a4 = reinterpret_cast<const vi4*>(acc + e0);
+    int64_t s = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const vi4 v = __builtin_nontemporal_load(a4 + i);
+        s += (int64_t)v.x + v.y + v.z + v.w;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if (rn_lane() == 0 && s != 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(st->esum + l), (unsigned long long)s);
+}
+
 __global__ void __launch_bounds__(64)
 k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
-           float* __restrict__ scale_next, uint32_t* __restrict__ vmax,
+           float* __restrict__ scale_next, FxStats* __restrict__ stats,
            int32_t* __restrict__ redo) {
     const int l = threadIdx.x;
+    uint32_t* vmax = stats->vmax;
     bool bad = false;
     if (l < RN_L) {
+        // net wrap of an int32 entry: the entries' exact sum differs from the
+        // records' sum by a multiple of 2^32 (the float record sum is good to
+        // far better than 2^31)
+        if (scale_cur[l] != 0.f &&
+            fabs((double)stats->esum[l] - stats->qsum[l]) > 2147483648.0)
+            bad = true;
+        stats->esum[l] = 0;
+        stats->qsum[l] = 0.0;
         const uint32_t vb = vmax[l];
         const float sc = scale_cur[l];
         float nx = sc;                                   // no records this step: keep
         if (vb >= 0x7f800000u) {                         // inf / NaN record
             nx = 0.f;
-            bad = sc != 0.f;
+            bad = bad || sc != 0.f;
         } else if (vb != 0u) {
             const float v = __uint_as_float(vb);
-            bad = sc != 0.f && v * sc >= 4194304.f;      // 2^22 units
+            bad = bad || (sc != 0.f && v * sc >= 4194304.f);   // 2^22 units
             int e;
             frexpf(v, &e);                               // v < 2^e
             nx = scalbnf(1.0f, max(-126, min(126, 19 - e)));
@@ -1853,7 +1910,11 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
     }
     FxGrad F{};
-    F.acc = fx_acc; F.scale = fx_scale; F.vmax = fx_vmax; F.redo = fx_redo;
+    F.acc = fx_acc; F.scale = fx_scale; F.redo = fx_redo;
+    if (fx_vmax) {
+        F.vmax = reinterpret_cast<FxStats*>(fx_vmax)->vmax;
+        F.qsum = reinterpret_cast<FxStats*>(fx_vmax)->qsum;
+    }
     const dim3 blk(BWD_WAVES * 64);
     if (fx_mode == 2) {
         k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
@@ -1960,7 +2021,10 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
         RN_CHECK_ARG(level_offset[l] % 8 == 0, "level offsets must be multiples of 8 entries");
     }
     hipStream_t st = (hipStream_t)stream;
-    k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, fx_vmax, fx_redo);
+    FxStats* stats = reinterpret_cast<FxStats*>(fx_vmax);
+    if (hashed)
+        k_fx_esum<<<dim3(64, RN_L), 256, 0, st>>>(gm, hashed, fx_acc, stats);
+    k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo);
     RN_CHECK_LAUNCH();
     if (first < RN_L) {
         const int64_t e0 = 2 * (int64_t)level_offset[first];

@@ -311,13 +311,21 @@ k_field_density(FieldArgs a, float* __restrict__ feat_out) {
 // ---------------------------------------------------------------------------
 // Sampled occupancy-grid update on the device (networks.py:345-409 with
 // warmup False, all K sub-NeRFs and C cascades per launch, no host sync).
-// Cells: per (sub-NeRF k, cascade c) M uniform cells and M cells drawn
-// uniformly among those with density > threshold, jittered in the cell; the
-// draws come from a counter-based hash of (seed, k, c, i, stream) instead of
-// torch's generator (same distribution; identical on every rank for the same
-// seed, which is what ray-batch data parallelism needs).
+// The reference draws, per (sub-NeRF k, cascade c), M = G^3/4 uniform cells
+// and M cells uniformly among those with density > threshold (with
+// replacement), jitters each in its cell and evaluates sigma there.  What the
+// update keeps of a cell is the max over its draws, so only the NUMBER of
+// draws per cell and their jitters matter: here every cell j gets
+// n_j = Poisson(M / G^3) + [occupied] Poisson(M / n_occupied) draws (the
+// limit of the multinomial counts; hit rates 1 - e^-1/4 and 1 - e^-(1/4 +
+// M/n_o) as the reference's), from a counter-based hash of (seed, k, c, j)
+// instead of torch's generator (identical on every rank for the same seed).
+// The draws are listed in cell (Morton) order and evaluated in that order, so
+// consecutive samples share grid lines as the warm-up's ordered sweep does
+// (random placement cost ~2x per sample: DESIGN.md §4).
 // ---------------------------------------------------------------------------
-#define DU_BLK 1024        // elements per compaction block (G^3 is a multiple)
+#define DU_BLK 1024        // cells per counting block (G^3 is a multiple)
+#define DU_DUP_MAX 31      // draws of one cell kept (5 bits of the list entry)
 
 __device__ __forceinline__ uint64_t du_mix(uint64_t z) {      // splitmix64 finaliser
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -330,12 +338,30 @@ __device__ __forceinline__ uint32_t du_hash(uint64_t seed, uint32_t seg, uint32_
 }
 __device__ __forceinline__ float du_unit(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
 
+// a Poisson(lam) count from the uniform words h (inverse CDF below rate 16;
+// above it the normal approximation, Box-Muller with h2), capped
+__device__ __forceinline__ uint32_t du_poisson(float lam, uint32_t h, uint32_t h2) {
+    if (!(lam > 0.f)) return 0u;
+    if (lam < 16.f) {
+        const float u = du_unit(h);
+        float p = expf(-lam), cdf = p;
+        uint32_t k = 0;
+        while (u > cdf && k < DU_DUP_MAX) { ++k; p *= lam / (float)k; cdf += p; }
+        return k;
+    }
+    const float u1 = fmaxf(du_unit(h), 1.0f / 16777216.0f), u2 = du_unit(h2);
+    const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530718f * u2);
+    const float v = floorf(lam + sqrtf(lam) * z + 0.5f);
+    return v <= 0.f ? 0u : (uint32_t)fminf(v, (float)DU_DUP_MAX);
+}
+
 struct DensityUpd {
     const float* const* grids;      // [K] -> (C, G3) density grids
     uint8_t* const* bitfields;      // [K] -> C G3 / 8 bytes
     float* tmp;                     // (K, C, G3) sampled sigma, zero on entry
-    int32_t* occ;                   // (K C G3) occupied cells, segment-ordered
-    int32_t* blk;                   // (K C G3 / DU_BLK + 1) per-block counts -> offsets
+    uint32_t* list;                 // (K C G3) draws, cell-ordered: cell | d << 21 | c << 26
+    int32_t* blk;                   // (K C G3 / DU_BLK + 1) occupied counts -> offsets
+    int32_t* dblk;                  // (K C G3 / DU_BLK + 1) draw counts -> offsets
     float* part;                    // (K, DU_PART, 2) partial sums / counts of positives
     float* thr_out;                 // [K] packbits threshold min(mean, thr)
     uint64_t seed;
@@ -362,60 +388,91 @@ k_du_count(DensityUpd u) {
     if (threadIdx.x == 0) u.blk[b] = sN;
 }
 
-// 2. exclusive scan of the block counts (one block, fixed order)
+// 2. exclusive scan of per-block counts (one block, fixed order); v[nb] = total
 __global__ void __launch_bounds__(1024)
-k_du_scan(DensityUpd u, int nb) {
+k_du_scan(int32_t* __restrict__ v, int nb) {
     __shared__ int sPart[1024];
     const int t = threadIdx.x, per = (nb + 1023) / 1024;
     int acc = 0;
-    for (int j = 0; j < per; ++j) { const int q = t * per + j; if (q < nb) acc += u.blk[q]; }
+    for (int j = 0; j < per; ++j) { const int q = t * per + j; if (q < nb) acc += v[q]; }
     sPart[t] = acc;
     __syncthreads();
     for (int off = 1; off < 1024; off <<= 1) {           // Hillis-Steele, inclusive
-        const int v = t >= off ? sPart[t - off] : 0;
+        const int x = t >= off ? sPart[t - off] : 0;
         __syncthreads();
-        sPart[t] += v;
+        sPart[t] += x;
         __syncthreads();
     }
     int run = t ? sPart[t - 1] : 0;
     for (int j = 0; j < per; ++j) {
         const int q = t * per + j;
-        if (q < nb) { const int v = u.blk[q]; u.blk[q] = run; run += v; }
+        if (q < nb) { const int x = v[q]; v[q] = run; run += x; }
     }
-    if (t == 1023) u.blk[nb] = sPart[1023];
+    if (t == 1023) v[nb] = sPart[1023];
 }
 
-// 3. ordered write of the occupied cells: segment-relative cell index j
+// draws of cell j of segment seg (the occupied part needs the segment's count)
+__device__ __forceinline__ uint32_t du_draws(const DensityUpd& u, int64_t seg, uint32_t j,
+                                             bool occupied, float lam_o) {
+    const uint32_t n0 = du_poisson(0.25f, du_hash(u.seed, (uint32_t)seg, j, 0), 0u);   // M / G^3
+    const uint32_t n1 = occupied ? du_poisson(lam_o, du_hash(u.seed, (uint32_t)seg, j, 1),
+                                              du_hash(u.seed, (uint32_t)seg, j, 5))
+                                 : 0u;
+    return min(n0 + n1, (uint32_t)DU_DUP_MAX);
+}
+
+__device__ __forceinline__ float du_lam_occ(const DensityUpd& u, int64_t seg, int64_t seg_blocks) {
+    const int32_t no = u.blk[(seg + 1) * seg_blocks] - u.blk[seg * seg_blocks];
+    return no > 0 ? (float)u.M / (float)no : 0.f;
+}
+
+// 3. per-block count of draws.  MODE 0: counts -> dblk; MODE 1: the ordered
+// list (each lane writes its cell's draws at its prefix position)
+template <int MODE>
 __global__ void __launch_bounds__(256)
-k_du_write(DensityUpd u) {
+k_du_draws(DensityUpd u, int64_t cap) {
     const int64_t G3 = (int64_t)u.G * u.G * u.G, seg_blocks = G3 / DU_BLK;
     const int64_t b = blockIdx.x;
     const int64_t seg = b / seg_blocks, k = seg / u.C, c = seg % u.C;
     const int64_t j0 = (b % seg_blocks) * DU_BLK;
     const float* g = u.grids[k] + c * G3 + j0;
+    const float lam_o = du_lam_occ(u, seg, seg_blocks);
     __shared__ int sWave[4];
-    int base = u.blk[b];
+    int64_t base = MODE ? u.dblk[b] : 0;
+    int total = 0;
     for (int j = 0; j < DU_BLK; j += blockDim.x) {
-        const bool o = g[j + threadIdx.x] > u.thr;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(o);
+        const uint32_t cell = (uint32_t)(j0 + j + threadIdx.x);
+        const int n = (int)du_draws(u, seg, cell, g[j + threadIdx.x] > u.thr, lam_o);
+        if (MODE == 0) { total += n; continue; }
+        const int incl = rn_wave_incl_sum_i(n);
         const int w = threadIdx.x / RN_WAVE;
-        if (rn_lane() == 0) sWave[w] = __builtin_popcountll(m);
+        if (rn_lane() == 63) sWave[w] = incl;
         __syncthreads();
         int before = 0;
         for (int q = 0; q < w; ++q) before += sWave[q];
         const int tot = sWave[0] + sWave[1] + sWave[2] + sWave[3];
-        const int r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        if (o) u.occ[base + before + r] = (int32_t)(j0 + j + threadIdx.x);
+        const int64_t p0 = base + before + incl - n;
+        for (int d = 0; d < n; ++d)
+            if (p0 + d < cap)
+                u.list[p0 + d] = cell | ((uint32_t)d << 21) | ((uint32_t)c << 26);
         base += tot;
         __syncthreads();
     }
+    if (MODE == 0) {
+        __shared__ int sN;
+        if (threadIdx.x == 0) sN = 0;
+        __syncthreads();
+        total = (int)rn_wave_sum((float)total);
+        if (rn_lane() == 0) atomicAdd(&sN, total);
+        __syncthreads();
+        if (threadIdx.x == 0) u.dblk[b] = sN;
+    }
 }
 
-// 4. draw, jitter, sigma (grid + geo MLP, as k_field_density) and scatter-max
-// of sample i of segment (k, c): i < M uniform, else occupied (skipped when
-// the segment has no occupied cell).  blockIdx.y = k.
+// 4. the listed draws of sub-NeRF k (blockIdx.y), in cell order: jitter,
+// sigma (grid + geo MLP, as k_field_density), scatter-max per cell
 __global__ void __launch_bounds__(256)
-k_du_sample(FieldArgs a, DensityUpd u) {
+k_du_sample(FieldArgs a, DensityUpd u, int64_t cap) {
     __shared__ __attribute__((aligned(16))) rn_half sW[8 * RN_FRAG_HALFS];
     __shared__ LvTab sT;
     const int k = blockIdx.y;
@@ -423,7 +480,9 @@ k_du_sample(FieldArgs a, DensityUpd u) {
     lv_stage(sT, a.gm);
     __syncthreads();
     const int64_t G3 = (int64_t)u.G * u.G * u.G, seg_blocks = G3 / DU_BLK;
-    const int64_t per_seg = 2 * (int64_t)u.M, n = per_seg * u.C;
+    const int64_t lo = min((int64_t)u.dblk[(int64_t)k * u.C * seg_blocks], cap);
+    const int64_t hi = min((int64_t)u.dblk[(int64_t)(k + 1) * u.C * seg_blocks], cap);
+    const int64_t n = hi - lo;
     const int64_t n_tiles = (n + 31) / 32;
     const int waves = blockDim.x / RN_WAVE;
     const int lane = rn_lane(), cl = lane & 31, h = lane >> 5;
@@ -432,33 +491,20 @@ k_du_sample(FieldArgs a, DensityUpd u) {
          tile += (int64_t)gridDim.x * waves) {
         rn_lds_order();
         const int64_t q = tile * 32 + cl;
-        bool valid = q < n;
-        const int c = valid ? (int)(q / per_seg) : 0;
-        const uint32_t i = valid ? (uint32_t)(q % per_seg) : 0u;
+        const bool valid = q < n;
+        const uint32_t e = valid ? u.list[lo + q] : 0u;
+        const uint32_t cell = e & 0x1fffffu, d = (e >> 21) & 31u;
+        const int c = (int)(e >> 26);
         const int seg = k * u.C + c;
-        uint32_t cell = 0;
-        if (valid) {
-            if (i < (uint32_t)u.M) {
-                cell = du_hash(u.seed, seg, i, 0) & (uint32_t)(G3 - 1);     // G3 = 2^21
-            } else {
-                const int32_t o0 = u.blk[(int64_t)seg * seg_blocks];
-                const int32_t no = u.blk[(int64_t)(seg + 1) * seg_blocks] - o0;
-                if (no > 0) {
-                    const uint32_t r = (uint32_t)(((uint64_t)du_hash(u.seed, seg, i, 1) * (uint32_t)no) >> 32);
-                    cell = (uint32_t)u.occ[o0 + r];
-                } else {
-                    valid = false;
-                }
-            }
-        }
         // networks.py:386-391: cell centre of cascade c, jittered by +-half a cell
         const float sc = fminf(scalbnf(1.0f, c - 1), u.scale);
         const float hgs = sc / u.G;
         const float gm1 = (float)(u.G - 1);
         const float cx = (float)rn_morton3d_invert(cell), cy = (float)rn_morton3d_invert(cell >> 1),
                     cz = (float)rn_morton3d_invert(cell >> 2);
-        const float jx = du_unit(du_hash(u.seed, seg, i, 2)), jy = du_unit(du_hash(u.seed, seg, i, 3)),
-                    jz = du_unit(du_hash(u.seed, seg, i, 4));
+        const uint32_t di = (cell << 5) | d;
+        const float jx = du_unit(du_hash(u.seed, seg, di, 2)), jy = du_unit(du_hash(u.seed, seg, di, 3)),
+                    jz = du_unit(du_hash(u.seed, seg, di, 4));
         const float x = ((cx / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jx * 2.0f - 1.0f) * hgs;
         const float y = ((cy / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jy * 2.0f - 1.0f) * hgs;
         const float z = ((cz / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jz * 2.0f - 1.0f) * hgs;
@@ -477,7 +523,7 @@ k_du_sample(FieldArgs a, DensityUpd u) {
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) gg = rn_mfma(rn_frag(sW, 4 + qq), h1[qq], gg);
         if (valid && h == 0) {
-            // duplicate cells keep their max (deterministic, as rn_scatter_max)
+            // duplicate draws of a cell keep their max (deterministic, as rn_scatter_max)
             const float sig = expf(gg[8]);
             atomicMax(reinterpret_cast<int*>(u.tmp) + (int64_t)seg * G3 + cell,
                       __float_as_int(fmaxf(sig, 0.0f)));
@@ -594,33 +640,39 @@ int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, 
                               const float* level_scale, const float* xyz_min, const float* extent,
                               const void* frags, float* tmp, int32_t* occ, int32_t* blk,
                               float* part, float* thr_out, void* stream) {
-    RN_CHECK_ARG(n_models >= 1 && cascades >= 1 && grid_size == 128, "bad sizes (grid_size 128)");
+    RN_CHECK_ARG(n_models >= 1 && cascades >= 1 && cascades <= 32 && grid_size == 128,
+                 "bad sizes (grid_size 128, cascades <= 32)");
     RN_CHECK_ARG(grid_ptrs && bitfield_ptrs && grid_f16 && level_offset && level_hsize &&
                  level_res && level_scale && xyz_min && extent && frags && tmp && occ && blk &&
                  part && thr_out, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
+    const int64_t G3 = (int64_t)grid_size * grid_size * grid_size;
+    const int64_t n_all = (int64_t)n_models * cascades * G3;
+    const int nb = (int)(n_all / DU_BLK);
     DensityUpd u{};
     u.grids = (const float* const*)grid_ptrs; u.bitfields = (uint8_t* const*)bitfield_ptrs;
-    u.tmp = tmp; u.occ = occ; u.blk = blk; u.part = part; u.thr_out = thr_out;
+    u.tmp = tmp; u.list = (uint32_t*)occ; u.blk = blk; u.dblk = blk + nb + 1;
+    u.part = part; u.thr_out = thr_out;
     u.seed = seed; u.K = n_models; u.C = cascades; u.G = grid_size;
-    const int64_t G3 = (int64_t)grid_size * grid_size * grid_size;
     u.M = (int)(G3 / 4);                                  // networks.py:378: grid_size**3 // 4
     u.thr = density_threshold; u.decay = decay; u.scale = scale;
     hipStream_t st = (hipStream_t)stream;
-    const int64_t n_all = (int64_t)n_models * cascades * G3;
-    const int nb = (int)(n_all / DU_BLK);
     if (hipMemsetAsync(tmp, 0, sizeof(float) * n_all, st) != hipSuccess) {
         rn_set_error("%s: memset failed", __func__);
         return 2;
     }
     k_du_count<<<nb, 256, 0, st>>>(u);
-    k_du_scan<<<1, 1024, 0, st>>>(u, nb);
-    k_du_write<<<nb, 256, 0, st>>>(u);
+    k_du_scan<<<1, 1024, 0, st>>>(u.blk, nb);
+    k_du_draws<0><<<nb, 256, 0, st>>>(u, n_all);
+    k_du_scan<<<1, 1024, 0, st>>>(u.dblk, nb);
+    k_du_draws<1><<<nb, 256, 0, st>>>(u, n_all);
+    // expected draws: 2 M per (sub-NeRF, cascade); the kernel strides over
+    // whatever the device-side count is
     const int64_t tiles = (2 * (int64_t)u.M * cascades + 31) / 32;
     const int sb = (int)(tiles / 4 + 1 < 2048 ? tiles / 4 + 1 : 2048);
-    k_du_sample<<<dim3(sb, n_models), 256, 0, st>>>(a, u);
+    k_du_sample<<<dim3(sb, n_models), 256, 0, st>>>(a, u, n_all);
     k_du_decay<<<dim3(DU_PART, n_models), 256, 0, st>>>(u);
     k_du_mean<<<n_models, 64, 0, st>>>(u);
     k_du_pack<<<dim3(nblk(cascades * G3 / 8, 256), n_models), 256, 0, st>>>(u);

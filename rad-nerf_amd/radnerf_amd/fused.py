@@ -80,11 +80,12 @@ class Workspace:
         """Fixed-point grid-gradient state (rn_grid_fx_fold): int32 sums (n,
         zero between steps), per-level scales (2, 16) (current / next, swapped
         by fx_i each step; zeros = fp32 until the first step has measured the
-        records), per-level record maxima (16,) and the redo flag."""
+        records), the per-level statistics block (384 B: record maxima, record
+        sums, entry sums; include/radnerf.h) and the redo flag."""
         if getattr(self, "_fx", None) is None or self._fx[0].numel() != n:
             z = dict(device=device, dtype=torch.int32)
             self._fx = (torch.zeros(n, **z), torch.zeros(2, 16, device=device),
-                        torch.zeros(16, **z), torch.zeros(1, **z))
+                        torch.zeros(96, **z), torch.zeros(1, **z))
             self.fx_i = 0
         return self._fx
 

@@ -416,7 +416,8 @@ class MNGP(nn.Module):
         if du is None or du["tmp"].numel() != n or du["tmp"].device != dev:
             du = {"tmp": torch.empty(n, device=dev),
                   "occ": torch.empty(n, device=dev, dtype=torch.int32),
-                  "blk": torch.empty(n // 1024 + 1, device=dev, dtype=torch.int32),
+                  # per-block occupied counts | per-block draw counts (scanned in place)
+                  "blk": torch.empty(2 * (n // 1024 + 1), device=dev, dtype=torch.int32),
                   "part": torch.empty(K * 1024, device=dev),
                   "thr": torch.empty(K, device=dev)}
             self._du = du

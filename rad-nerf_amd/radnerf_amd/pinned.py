@@ -67,9 +67,16 @@ class PinnedMLRenderer(FusedMLRenderer):
     (B, K)).  Gradients: pass the views of a dist.GradAllReduce over
     [grid, mlp_params, gate] and call reduce(average=False) after backward."""
 
-    def __init__(self, model, gating_net, n_rays, group=None, device=None, **kw):
+    def __init__(self, model, gating_net, n_rays, group=None, device=None, sim=None, **kw):
+        """sim=(rank, world): run rank `rank`'s share of a `world`-rank layout
+        in this one process (bench.py --pinned-sim: its sub-NeRFs over all B
+        rays, the gate backward if rank 0), the all-gather replaced by local
+        copies of this rank's rows (the other ranks' rows are stand-ins)."""
         self.group = group
-        if dist.is_initialized():
+        self.simulated = sim is not None
+        if self.simulated:
+            rank, world = sim
+        elif dist.is_initialized():
             rank, world = dist.get_rank(group), dist.get_world_size(group)
         else:
             rank, world = 0, 1
@@ -107,7 +114,12 @@ class PinnedMLRenderer(FusedMLRenderer):
         pk[:, :B].copy_(w.opacity_k)
         pk[:, B:2 * B].copy_(w.depth_k)
         pk[:, 2 * B:].copy_(w.rgb_k.view(-1, 3 * B))
-        all_gather_rows(self._gathered, pk, self.group)
+        if self.simulated:
+            # one process stands in for all ranks: every rank's rows = ours
+            self._gathered.view(self.world, *pk.shape).copy_(
+                pk.unsqueeze(0).expand(self.world, *pk.shape))
+        else:
+            all_gather_rows(self._gathered, pk, self.group)
         g = self._gathered
         self.opacity_all.copy_(g[:, :B])
         self.depth_all.copy_(g[:, B:2 * B])
