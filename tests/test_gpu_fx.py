@@ -95,8 +95,9 @@ def test_fx_entry_wrap_sets_redo(cuda):
     """an int32 entry can wrap with every record under the 2^22-
     unit growth bound when many same-sign records land on it.  Here all 8192
     rays are the same ray (K = 2) with positive seeds: the coarse hashed
-    levels' entries take ~16k records each, and the step's scale is the one
-    the previous identical step measured (no growth).  The level's exact
+    levels' entries take ~16k records each, and the step's scale is 4x the
+    one the previous identical step measured ("just under the 8x redo
+    threshold": no record reaches 2^22 units).  The level's exact
     entry sum then differs from its record sum by a multiple of 2^32, the
     redo flag is set, and the result is the fp32 one."""
     B, K = 8192, 2
@@ -107,13 +108,19 @@ def test_fx_entry_wrap_sets_redo(cuda):
     r = get_renderer(m, g, B)
     _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)       # fp32: scales
     acc, scales, stats, redo = r.ws._fx
-    cur = scales[r.ws.fx_i].clone()
+    cur = scales[r.ws.fx_i]
     hashed, lv = _hashed(0.5)
-    # the test's premise: some entry's exact integer sum exceeds the int32 range
+    # the scale the previous step measured maps the largest record to
+    # [2^18, 2^19) units; 4x that keeps every record under 2^21 units, below
+    # the 2^22-unit growth bound (the vmax check does not fire)
+    f = 4.0
     g_e = g32[0].view(-1, 2)
-    over = [l for l in hashed
-            if float(_level(g_e, lv, l).abs().max()) * float(cur[l]) > 2.0 ** 31]
-    assert over, "no entry sum beyond 2^31 units: the test needs more records per entry"
+    units = {l: float(_level(g_e, lv, l).abs().max()) * float(cur[l]) * f for l in hashed}
+    # the test's premise: some entry's exact integer sum exceeds the int32 range
+    over = [l for l in hashed if units[l] > 2.0 ** 31]
+    assert over, {l: f"{u:.3g}" for l, u in units.items()}
+    with torch.no_grad():
+        cur[hashed] = cur[hashed] * f
     _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
     assert int(redo[0]) == 1
     for l in range(16):
