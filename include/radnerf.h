@@ -234,15 +234,15 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * 0 for fp32 atomics into grid_grad (dense levels, first step); fx_vmax: the
  * 384-B per-level statistics block, zero before the first step: u32 vmax[16]
  * (the kernel atomic-maxes the bits of each level's largest |record|),
- * u32 pad[16], f64 qsum[16] (the sum of each level's integer records),
+ * u32 pad[16], i64 qsum[16] (the exact sum of each level's integer records),
  * i64 esum[16] (rn_grid_fx_fold: the exact sum of the level's int32 entries).
  * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
  * memory side serves them ~27 % faster than f32 adds), so those levels'
  * gradients are order-independent and bitwise reproducible.
  * rn_grid_fx_fold then (1) sets *fx_redo when a level's largest record reached
  * 2^22 units or was not finite, or when the level's entry sum differs from its
- * record sum by more than 2^31 (an int32 entry wrapped: many same-sign
- * records), writes the next step's scales
+ * record sum (an int32 entry wrapped: many same-sign records), writes the
+ * next step's scales
  * (2^(19 - e), |record| < 2^e; dense levels 0) to fx_scale_next and clears
  * the statistics, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
  * and re-zeroes fx_acc.  The caller then launches rn_field_bwd_merged with

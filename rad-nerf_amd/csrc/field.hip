@@ -290,16 +290,17 @@ struct Walk2 {
     // the largest |record| issued for each, as float bits (NaN/inf included)
     float fxA, fxB;
     uint32_t vmA, vmB;
-    // ... and the sum of the integer records issued for each (float: the
-    // net-wrap check of rn_grid_fx_fold needs it to well within 2^31)
-    float sqA, sqB;
+    // ... and the exact sum of the integer records issued for each (the
+    // net-wrap check of rn_grid_fx_fold)
+    int64_t sqA, sqB;
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     W.ring = ring; W.head = 0; W.tail = 0; W.pend = 0;
     W.ex0 = W2_NONE; W.ex1 = W2_NONE; W.ey = 0; W.ez = 0; W.cur0 = 0; W.cur1 = 0;
     W.a00 = W.a01 = W.a10 = W.a11 = 0.f;
-    W.sqA = W.sqB = 0.f;
+    // (vmA/vmB and sqA/sqB are the kernel's: walk2_end re-begins the walk
+    // after its last issue, so they are not reset here)
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
     W.offA = W.offB = 0;
 }
@@ -343,13 +344,14 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // use fp32 atomics.
 // An int32 entry can still wrap with every record under 2^22 units (many
 // same-sign records on one entry); the kernel therefore also sums each
-// level's integer records (per lane in float, per wave in double), and
-// rn_grid_fx_fold sums the level's int32 entries exactly: a wrapped entry
-// makes the two differ by a multiple of 2^32, which sets the redo flag too.
+// level's integer records exactly (int64), and rn_grid_fx_fold sums the
+// level's int32 entries exactly: a wrapped entry makes the two differ by a
+// multiple of 2^32, which sets the redo flag too.  (A float sum of the
+// records is not enough: its rounding reached 2^31 on trained grids.)
 struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats block
     uint32_t vmax[RN_L];   // largest |record| this step (float bits, atomicMax)
     uint32_t pad[RN_L];
-    double qsum[RN_L];     // sum of the issued integer records
+    int64_t qsum[RN_L];    // sum of the issued integer records
     int64_t esum[RN_L];    // sum of the int32 entries (rn_grid_fx_fold)
 };
 
@@ -357,7 +359,7 @@ struct FxGrad {
     int32_t* acc;              // int32 [entries][2]
     const float* scale;        // [RN_L] 2^e_l, 0 = fp32 atomics for the level
     uint32_t* vmax;            // FxStats::vmax
-    double* qsum;              // FxStats::qsum
+    int64_t* qsum;             // FxStats::qsum
     const int32_t* redo;       // GM 3: the launch runs only when *redo != 0
     __amdgpu_buffer_rsrc_t rs; // over acc (built in the kernel)
 };
@@ -410,7 +412,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             int q;
             asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
-            if (odd) W.sqB += (float)q; else W.sqA += (float)q;
+            if (odd) W.sqB += (int64_t)q; else W.sqA += (int64_t)q;
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -983,7 +985,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     // fixed point: this wave's two levels' scales (wave-uniform) and maxima
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
-    float sqA = 0.f, sqB = 0.f;
+    int64_t sqA = 0, sqB = 0;
     if (GM >= 2) {
         fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
         fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
@@ -1147,7 +1149,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     if (GM == 2) {                               // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
         vmB = rn_wave_max_u32(vmB);
-        double dA = (double)sqA, dB = (double)sqB;
+        int64_t dA = sqA, dB = sqB;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             dA += __shfl_xor(dA, off);
@@ -1156,8 +1158,10 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         if (rn_lane() == 0) {
             if (vmA) atomicMax(F.vmax + wid, vmA);
             if (vmB) atomicMax(F.vmax + RN_L - 1 - wid, vmB);
-            if (dA != 0.0) atomicAdd(F.qsum + wid, dA);
-            if (dB != 0.0) atomicAdd(F.qsum + RN_L - 1 - wid, dB);
+            if (dA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + wid),
+                                   (unsigned long long)dA);
+            if (dB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + RN_L - 1 - wid),
+                                   (unsigned long long)dB);
         }
     }
     // ---- flush every model's dW (the current one from registers)
@@ -1377,13 +1381,10 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
     bool bad = false;
     if (l < RN_L) {
         // net wrap of an int32 entry: the entries' exact sum differs from the
-        // records' sum by a multiple of 2^32 (the float record sum is good to
-        // far better than 2^31)
-        if (scale_cur[l] != 0.f &&
-            fabs((double)stats->esum[l] - stats->qsum[l]) > 2147483648.0)
-            bad = true;
+        // records' exact sum (by a multiple of 2^32)
+        if (scale_cur[l] != 0.f && stats->esum[l] != stats->qsum[l]) bad = true;
         stats->esum[l] = 0;
-        stats->qsum[l] = 0.0;
+        stats->qsum[l] = 0;
         const uint32_t vb = vmax[l];
         const float sc = scale_cur[l];
         float nx = sc;                                   // no records this step: keep
@@ -2023,7 +2024,7 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
     hipStream_t st = (hipStream_t)stream;
     FxStats* stats = reinterpret_cast<FxStats*>(fx_vmax);
     if (hashed)
-        k_fx_esum<<<dim3(64, RN_L), 256, 0, st>>>(gm, hashed, fx_acc, stats);
+        k_fx_esum<<<dim3(256, RN_L), 256, 0, st>>>(gm, hashed, fx_acc, stats);
     k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo);
     RN_CHECK_LAUNCH();
     if (first < RN_L) {
