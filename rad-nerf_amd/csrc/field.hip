@@ -335,14 +335,14 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // against 20.9 for f32 (profiles/r01/atomic_probe.json), and the sums are
 // exact, so these levels' gradients are bitwise reproducible.  e_l comes from
 // the previous step's largest record of the level (rn_grid_fx_fold): that
-// record maps to < 2^19 units, leaving 2^12 max-size records of headroom per
+// record maps to < 2^23 units, leaving 2^8 max-size records of headroom per
 // entry (an entry of a hashed level takes ~77 records per C3 step, of mixed
 // sign).  The kernel records this step's largest |record| per level; when it
-// exceeds 2^22 units (8x growth) or is not finite, rn_grid_fx_fold discards
+// exceeds 2^28 units (32x growth) or is not finite, rn_grid_fx_fold discards
 // the fixed-point sums and the GM 3 launch redoes the grid scatter in fp32.
 // Dense levels (few requests: merged per ray) and the first step (scale 0)
 // use fp32 atomics.
-// An int32 entry can still wrap with every record under 2^22 units (many
+// An int32 entry can still wrap with every record under 2^28 units (many
 // same-sign records on one entry); the kernel therefore also sums each
 // level's integer records exactly (int64), and rn_grid_fx_fold sums the
 // level's int32 entries exactly: a wrapped entry makes the two differ by a
@@ -1344,13 +1344,6 @@ k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
     carry[i] = 0;
 }
 
-// Fixed-point step bookkeeping (one wave): redo flag of this step, the next
-// step's per-level scales from this step's largest records, vmax reset.
-// Scale 2^(19 - e) with |record| < 2^e: the largest record maps to < 2^19
-// units.  A level whose largest record reached 2^22 units under the current
-// scale (8x growth since the step the scale came from), or a non-finite one,
-// sets the redo flag: rn_grid_fx_fold then discards the fixed-point sums and
-// the GM 3 launch recomputes the grid gradient in fp32.
 // Exact per-level sum of the int32 entries (int64), for the net-wrap check.
 __global__ void __launch_bounds__(256)
 k_fx_esum(GridMeta gm, uint32_t hashed_mask, const int32_t* __restrict__ acc,
@@ -1372,6 +1365,20 @@ k_fx_esum(GridMeta gm, uint32_t hashed_mask, const int32_t* __restrict__ acc,
         atomicAdd(reinterpret_cast<unsigned long long*>(st->esum + l), (unsigned long long)s);
 }
 
+// Fixed-point step bookkeeping (one wave): redo flag of this step, the next
+// step's per-level scales from this step's largest records, statistics reset.
+// Scale 2^(FX_TARGET_BITS - e) with |record| < 2^e: the largest record maps
+// to < 2^23 units.  A level whose largest record reached 2^28 units under the
+// current scale (32x growth since the step the scale came from), or a
+// non-finite one, or whose entries wrapped (entry sum != record sum), sets the
+// redo flag: rn_grid_fx_fold then discards the fixed-point sums and the GM 3
+// launch recomputes the grid gradient in fp32.
+// Headroom measured on C3 over 12 Adam steps (tools/fx_diag.py): the largest
+// |entry| stays within 2^1.2 of the largest record, so at 2^23 units it sits
+// ~2^7 below the int32 range; the unit 2^-23 of the level's largest record
+// leaves 0.01 % of the non-zero fp32 entries at 0 (2^19: 0.15 %).
+#define FX_TARGET_BITS 23
+#define FX_GROWTH_UNITS 268435456.f       // 2^28
 __global__ void __launch_bounds__(64)
 k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
            float* __restrict__ scale_next, FxStats* __restrict__ stats,
@@ -1393,10 +1400,10 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
             bad = bad || sc != 0.f;
         } else if (vb != 0u) {
             const float v = __uint_as_float(vb);
-            bad = bad || (sc != 0.f && v * sc >= 4194304.f);   // 2^22 units
+            bad = bad || (sc != 0.f && v * sc >= FX_GROWTH_UNITS);
             int e;
             frexpf(v, &e);                               // v < 2^e
-            nx = scalbnf(1.0f, max(-126, min(126, 19 - e)));
+            nx = scalbnf(1.0f, max(-126, min(126, FX_TARGET_BITS - e)));
         }
         if (!((hashed_mask >> l) & 1u)) nx = 0.f;       // dense levels: fp32 atomics
         scale_next[l] = nx;

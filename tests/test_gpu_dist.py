@@ -82,3 +82,24 @@ def test_bucketed_adam_epilogue_matches_plain(tmp_path):
     res = _run_ranks("adam_worker.py", tmp_path / "adam.json", timeout=100)
     assert res["world"] == 2
     assert res["same_params"] and res["same_moments"] and res["ranks_agree"], res
+
+
+def test_rccl_calls_world1(tmp_path):
+    """Every collective of the multi-GPU paths, issued through RCCL as they
+    issue it, in a one-rank RCCL group on GPU 0 (tests/rccl_worker.py): the
+    calls are legal for the backend (async bucket slices, tensor and object
+    all-gathers, f64 MAX, barrier) and leave the data as expected."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    out = tmp_path / "rccl.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()), RANK="0",
+               LOCAL_RANK="0", WORLD_SIZE="1")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "rccl_worker.py"), str(out)],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    res = json.loads(out.read_text())
+    assert res["backend"] == "nccl"
+    assert res["bucketed_allreduce_equal"] and res["buckets"] == 4
+    assert res["all_gather_rows_equal"]
+    assert res["all_gather_object"] == [{"rank": 0, "device": 0}]
+    assert res["max_f64"] == 1.25

@@ -62,9 +62,9 @@ def check_grads_vs_oracle(m, gf, ores, tag):
 
 
 # fixed point vs fp32 atomics, per hash level: the largest record of a level
-# maps to < 2^19 units, so a record of typical size carries ~1e-4 relative
-# rounding (measured max 3.7e-5 at scale 0.5, 1.2e-4 at scale 16; tcnn's own
-# half2 atomics round each add to 2^-11 ~ 4.9e-4)
+# maps to < 2^23 units (2^19 until round 2: measured max 3.7e-5 at scale 0.5,
+# 1.2e-4 at scale 16; tcnn's own half2 atomics round each add to 2^-11 ~
+# 4.9e-4)
 FX_LEVEL_TOL = 3e-4
 
 

@@ -6,6 +6,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "rad-nerf_amd")]
+import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from radnerf_amd import layout as LY  # noqa: E402
@@ -17,6 +18,7 @@ from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 
 def main():
     B, K, scale = int(sys.argv[1]) if len(sys.argv) > 1 else 8192, 2, 0.5
+    # usage: fx_diag.py [B] [steps] [adam]
     dev = torch.device("cuda", 0)
     model = MNGP(scale, size=K, seed=3).to(dev)
     gate = Ray_Gate(K, seed=4).to(dev)
@@ -45,12 +47,20 @@ def main():
 
     L.grid_fx_fold = fold
     lv = LY.grid_levels(scale)
-    for step in range(3):
+    from radnerf_amd.optim import FusedAdam
+    params = [model.xyz_encoder.params, model.mlp_params, gate.params]
+    opt = FusedAdam(params, lr=1e-2, eps=1e-15) if "adam" in sys.argv else None
+    n_steps = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    for step in range(n_steps):
         gg = torch.zeros_like(model.xyz_encoder.params)
         mg = torch.zeros_like(model.mlp_params)
         ag = torch.zeros_like(gate.params)
         _, _, _, gt, _ = r.forward(o, d, d, noise, bg, 1e-4, 0.0)
         r.backward(o, d, d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4, gg, mg, ag)
+        if opt is not None:
+            for p_, g_ in zip(params, (gg, mg, ag)):
+                p_.grad = g_
+            opt.step()
         torch.cuda.synchronize()
         st = cap["stats"]
         qsum = st[32:64].view(torch.int64)
@@ -59,8 +69,9 @@ def main():
         for l in range(16):
             a, n = int(lv["offset"][l]), int(lv["hsize"][l])
             es = int(acc[a:a + n].sum())
+            mx = int(acc[a:a + n].abs().max())
             print(f"  level {l:2d} scale {float(cap['scale'][l]):.3g}: entries {es} records "
-                  f"{int(qsum[l])} diff {es - int(qsum[l])}")
+                  f"{int(qsum[l])} diff {es - int(qsum[l])}; max |entry| 2^{np.log2(max(mx, 1)):.1f} units")
 
 
 if __name__ == "__main__":
