@@ -228,13 +228,14 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         int32_t* fx_acc, const float* fx_scale, uint32_t* fx_vmax,
                         const int32_t* fx_redo, int32_t fx_mode, void* stream);
 
-/* Fixed-point accumulation of the hashed levels' grid gradient (fx_mode 2,
- * the fused renderer's default; needs the encoding cache).  fx_acc: int32, one
+/* Fixed-point accumulation of the grid gradient (fx_mode 2, the fused
+ * renderer's default; needs the encoding cache).  fx_acc: int32, one
  * per grid_grad element, zero on entry; fx_scale [16] f32 per level: 2^e_l, or
- * 0 for fp32 atomics into grid_grad (dense levels, first step); fx_vmax: the
+ * 0 for fp32 atomics into grid_grad (the first step); fx_vmax: the
  * 384-B per-level statistics block, zero before the first step: u32 vmax[16]
  * (the kernel atomic-maxes the bits of each level's largest |record|),
- * u32 pad[16], i64 qsum[16] (the exact sum of each level's integer records),
+ * u32 emax[16] (rn_grid_fx_fold: the level's largest |int32 entry|),
+ * i64 qsum[16] (the exact sum of each level's integer records),
  * i64 esum[16] (rn_grid_fx_fold: the exact sum of the level's int32 entries).
  * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
  * memory side serves them ~27 % faster than f32 adds), so those levels'
@@ -243,7 +244,8 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * 2^28 units or was not finite, or when the level's entry sum differs from its
  * record sum (an int32 entry wrapped: many same-sign records), writes the
  * next step's scales
- * (2^(23 - e), |record| < 2^e; dense levels 0) to fx_scale_next and clears
+ * (2^(23 - e), |record| < 2^e, capped so the largest entry stays < 2^28 units;
+ * a dense level's first fixed-point step 2^(14 - e)) to fx_scale_next and clears
  * the statistics, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
  * and re-zeroes fx_acc.  The caller then launches rn_field_bwd_merged with
  * fx_mode 3 and the same fx_scale (fp32 redo of the fixed-point levels' grid

@@ -340,8 +340,10 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // sign).  The kernel records this step's largest |record| per level; when it
 // exceeds 2^28 units (32x growth) or is not finite, rn_grid_fx_fold discards
 // the fixed-point sums and the GM 3 launch redoes the grid scatter in fp32.
-// Dense levels (few requests: merged per ray) and the first step (scale 0)
-// use fp32 atomics.
+// The first step of a workspace (scale 0) uses fp32 atomics and measures the
+// records; the dense levels (few requests, but entries that sum hundreds of
+// records) go fixed point from then on with a scale capped by their largest
+// entry (k_fx_check).
 // An int32 entry can still wrap with every record under 2^28 units (many
 // same-sign records on one entry); the kernel therefore also sums each
 // level's integer records exactly (int64), and rn_grid_fx_fold sums the
@@ -350,7 +352,7 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // records is not enough: its rounding reached 2^31 on trained grids.)
 struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats block
     uint32_t vmax[RN_L];   // largest |record| this step (float bits, atomicMax)
-    uint32_t pad[RN_L];
+    uint32_t emax[RN_L];   // largest |int32 entry| this step (units; rn_grid_fx_fold)
     int64_t qsum[RN_L];    // sum of the issued integer records
     int64_t esum[RN_L];    // sum of the int32 entries (rn_grid_fx_fold)
 };
@@ -1344,32 +1346,42 @@ k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
     carry[i] = 0;
 }
 
-// Exact per-level sum of the int32 entries (int64), for the net-wrap check.
+// Exact per-level sum of the int32 entries (int64), for the net-wrap check,
+// and the level's largest |entry| (the next step's scale keeps it in range).
 __global__ void __launch_bounds__(256)
-k_fx_esum(GridMeta gm, uint32_t hashed_mask, const int32_t* __restrict__ acc,
+k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restrict__ acc,
           FxStats* __restrict__ st) {
     const int l = blockIdx.y;
-    if (!((hashed_mask >> l) & 1u)) return;
+    if (scale[l] == 0.f) return;                  // fp32 level this step: nothing in acc
     typedef int vi4 __attribute__((ext_vector_type(4)));
     const int64_t e0 = 2 * (int64_t)gm.offset[l], n4 = (2 * (int64_t)gm.hsize[l]) >> 2;
     const vi4* a4 = reinterpret_cast<const vi4*>(acc + e0);
     int64_t s = 0;
+    uint32_t mx = 0u;
+    auto uabs = [](int x) { return x < 0 ? 0u - (uint32_t)x : (uint32_t)x; };
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
          i += (int64_t)gridDim.x * blockDim.x) {
         const vi4 v = __builtin_nontemporal_load(a4 + i);
         s += (int64_t)v.x + v.y + v.z + v.w;
+        mx = max(max(mx, max(uabs(v.x), uabs(v.y))), max(uabs(v.z), uabs(v.w)));
     }
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-    // one atomic per block (per-wave atomics on the 10 level words serialised:
+    for (int off = 32; off > 0; off >>= 1) {
+        s += __shfl_xor(s, off);
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
+    }
+    // one atomic per block (per-wave atomics on the level words serialised:
     // 107 us for 16k of them)
     __shared__ int64_t sW[4];
+    __shared__ uint32_t sM[4];
     const int w = threadIdx.x / RN_WAVE;
-    if (rn_lane() == 0) sW[w] = s;
+    if (rn_lane() == 0) { sW[w] = s; sM[w] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int64_t t = (sW[0] + sW[1]) + (sW[2] + sW[3]);
+        const uint32_t m = max(max(sM[0], sM[1]), max(sM[2], sM[3]));
         if (t != 0) atomicAdd(reinterpret_cast<unsigned long long*>(st->esum + l), (unsigned long long)t);
+        if (m != 0u) atomicMax(st->emax + l, m);
     }
 }
 
@@ -1382,10 +1394,16 @@ k_fx_esum(GridMeta gm, uint32_t hashed_mask, const int32_t* __restrict__ acc,
 // redo flag: rn_grid_fx_fold then discards the fixed-point sums and the GM 3
 // launch recomputes the grid gradient in fp32.
 // Headroom measured on C3 over 12 Adam steps (tools/fx_diag.py): the largest
-// |entry| stays within 2^1.2 of the largest record, so at 2^23 units it sits
-// ~2^7 below the int32 range; the unit 2^-23 of the level's largest record
-// leaves 0.01 % of the non-zero fp32 entries at 0 (2^19: 0.15 %).
+// |entry| of a hashed level stays within 2^1.2 of its largest record, so at
+// 2^23 units it sits ~2^7 below the int32 range; the unit 2^-23 of the level's
+// largest record leaves 0.01 % of the non-zero fp32 entries at 0 (2^19:
+// 0.15 %).  A dense (coarse) level's entry sums up to hundreds of records, so
+// its scale is also capped by this step's largest |entry|: it maps to < 2^28
+// units (2^3 of headroom for growth); a dense level's first fixed-point step,
+// with no entry measured yet, maps its largest record to < 2^14 units.
 #define FX_TARGET_BITS 23
+#define FX_ENTRY_BITS 28
+#define FX_DENSE_FIRST_BITS 14
 #define FX_GROWTH_UNITS 268435456.f       // 2^28
 __global__ void __launch_bounds__(64)
 k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
@@ -1402,6 +1420,7 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
         stats->qsum[l] = 0;
         const uint32_t vb = vmax[l];
         const float sc = scale_cur[l];
+        const uint32_t em = stats->emax[l];
         float nx = sc;                                   // no records this step: keep
         if (vb >= 0x7f800000u) {                         // inf / NaN record
             nx = 0.f;
@@ -1411,17 +1430,25 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
             bad = bad || (sc != 0.f && v * sc >= FX_GROWTH_UNITS);
             int e;
             frexpf(v, &e);                               // v < 2^e
-            nx = scalbnf(1.0f, max(-126, min(126, FX_TARGET_BITS - e)));
+            int bits = FX_TARGET_BITS - e;
+            if (sc != 0.f && em != 0u) {                 // the largest entry stays < 2^28 units
+                int ee;
+                frexpf((float)em / sc, &ee);
+                bits = min(bits, FX_ENTRY_BITS - ee);
+            } else if (!((hashed_mask >> l) & 1u)) {     // dense level, no entry measured yet
+                bits = FX_DENSE_FIRST_BITS - e;
+            }
+            nx = scalbnf(1.0f, max(-126, min(126, bits)));
         }
-        if (!((hashed_mask >> l) & 1u)) nx = 0.f;       // dense levels: fp32 atomics
         scale_next[l] = nx;
         vmax[l] = 0u;
+        stats->emax[l] = 0u;
     }
     const uint64_t b = __builtin_amdgcn_ballot_w64(bad);
     if (l == 0) *redo = b ? 1 : 0;
 }
 
-// grid_grad += acc * 2^-e_l over the hashed levels' entries (elements
+// grid_grad += acc * 2^-e_l over the fixed-point levels' entries (elements
 // [e0, e1), 16-B aligned), acc = 0; with the redo flag set the sums are only
 // cleared (the fp32 redo adds the step's gradient instead).
 __global__ void __launch_bounds__(256)
@@ -2026,24 +2053,19 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
     RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
     GridMeta gm{};
     uint32_t hashed = 0;
-    int first = RN_L;
     for (int l = 0; l < RN_L; ++l) {
         gm.offset[l] = level_offset[l]; gm.hsize[l] = level_hsize[l]; gm.res[l] = level_res[l];
         const uint64_t r = level_res[l];
-        if (r * r * r > (uint64_t)level_hsize[l]) {
-            hashed |= 1u << l;
-            first = l < first ? l : first;
-        }
+        if (r * r * r > (uint64_t)level_hsize[l]) hashed |= 1u << l;
         RN_CHECK_ARG(level_offset[l] % 8 == 0, "level offsets must be multiples of 8 entries");
     }
     hipStream_t st = (hipStream_t)stream;
     FxStats* stats = reinterpret_cast<FxStats*>(fx_vmax);
-    if (hashed)
-        k_fx_esum<<<dim3(128, RN_L), 256, 0, st>>>(gm, hashed, fx_acc, stats);
+    k_fx_esum<<<dim3(128, RN_L), 256, 0, st>>>(gm, fx_scale_cur, fx_acc, stats);
     k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo);
     RN_CHECK_LAUNCH();
-    if (first < RN_L) {
-        const int64_t e0 = 2 * (int64_t)level_offset[first];
+    {   // every level (dense ones go fixed point from their second step)
+        const int64_t e0 = 2 * (int64_t)level_offset[0];
         const int64_t e1 = 2 * ((int64_t)level_offset[RN_L - 1] + level_hsize[RN_L - 1]);
         RN_CHECK_ARG(e1 % 4 == 0, "table size must be a multiple of 2 entries");
         const int64_t n4 = (e1 - e0) / 4;
