@@ -352,7 +352,7 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // records is not enough: its rounding reached 2^31 on trained grids.)
 struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats block
     uint32_t vmax[RN_L];   // largest |record| this step (float bits, atomicMax)
-    uint32_t emax[RN_L];   // largest |int32 entry| this step (units; rn_grid_fx_fold)
+    uint32_t emax[RN_L];   // largest |entry| this step, gradient units (float bits; rn_grid_fx_fold)
     int64_t qsum[RN_L];    // sum of the issued integer records
     int64_t esum[RN_L];    // sum of the int32 entries (rn_grid_fx_fold)
 };
@@ -1347,23 +1347,36 @@ k_igrad_to_f32(int64_t n, int32_t* __restrict__ lo, int32_t* __restrict__ carry,
 }
 
 // Exact per-level sum of the int32 entries (int64), for the net-wrap check,
-// and the level's largest |entry| (the next step's scale keeps it in range).
+// and the level's largest |entry| in gradient units (the next step's scale
+// keeps it in range): from the int32 entries of a fixed-point level, from
+// grid_grad for a level that went in as fp32 this step (the first step; an
+// upper bound when the caller accumulates several steps into grid_grad).
 __global__ void __launch_bounds__(256)
 k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restrict__ acc,
-          FxStats* __restrict__ st) {
+          const float* __restrict__ grad, FxStats* __restrict__ st) {
     const int l = blockIdx.y;
-    if (scale[l] == 0.f) return;                  // fp32 level this step: nothing in acc
+    const float sc = scale[l];
     typedef int vi4 __attribute__((ext_vector_type(4)));
     const int64_t e0 = 2 * (int64_t)gm.offset[l], n4 = (2 * (int64_t)gm.hsize[l]) >> 2;
-    const vi4* a4 = reinterpret_cast<const vi4*>(acc + e0);
     int64_t s = 0;
-    uint32_t mx = 0u;
+    uint32_t mx = 0u;           // fixed point: |int|; fp32 level: |float| bits
     auto uabs = [](int x) { return x < 0 ? 0u - (uint32_t)x : (uint32_t)x; };
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        const vi4 v = __builtin_nontemporal_load(a4 + i);
-        s += (int64_t)v.x + v.y + v.z + v.w;
-        mx = max(max(mx, max(uabs(v.x), uabs(v.y))), max(uabs(v.z), uabs(v.w)));
+    if (sc != 0.f) {
+        const vi4* a4 = reinterpret_cast<const vi4*>(acc + e0);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+             i += (int64_t)gridDim.x * blockDim.x) {
+            const vi4 v = __builtin_nontemporal_load(a4 + i);
+            s += (int64_t)v.x + v.y + v.z + v.w;
+            mx = max(max(mx, max(uabs(v.x), uabs(v.y))), max(uabs(v.z), uabs(v.w)));
+        }
+    } else {
+        const vi4* g4 = reinterpret_cast<const vi4*>(grad + e0);
+        for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
+             i += (int64_t)gridDim.x * blockDim.x) {
+            const vi4 v = __builtin_nontemporal_load(g4 + i);
+            mx = max(max(mx, max((uint32_t)v.x & 0x7fffffffu, (uint32_t)v.y & 0x7fffffffu)),
+                     max((uint32_t)v.z & 0x7fffffffu, (uint32_t)v.w & 0x7fffffffu));
+        }
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
@@ -1379,9 +1392,10 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
     __syncthreads();
     if (threadIdx.x == 0) {
         const int64_t t = (sW[0] + sW[1]) + (sW[2] + sW[3]);
-        const uint32_t m = max(max(sM[0], sM[1]), max(sM[2], sM[3]));
+        uint32_t m = max(max(sM[0], sM[1]), max(sM[2], sM[3]));
+        if (sc != 0.f) m = __float_as_uint((float)m / sc);     // units -> gradient units
         if (t != 0) atomicAdd(reinterpret_cast<unsigned long long*>(st->esum + l), (unsigned long long)t);
-        if (m != 0u) atomicMax(st->emax + l, m);
+        if (m != 0u && m < 0x7f800000u) atomicMax(st->emax + l, m);
     }
 }
 
@@ -1399,8 +1413,9 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 // largest record leaves 0.01 % of the non-zero fp32 entries at 0 (2^19:
 // 0.15 %).  A dense (coarse) level's entry sums up to hundreds of records, so
 // its scale is also capped by this step's largest |entry|: it maps to < 2^28
-// units (2^3 of headroom for growth); a dense level's first fixed-point step,
-// with no entry measured yet, maps its largest record to < 2^14 units.
+// units (2^3 of headroom for growth; the first step's entries are read from
+// the fp32 grid_grad); a dense level with no entry measured maps its largest
+// record to < 2^14 units.
 #define FX_TARGET_BITS 23
 #define FX_ENTRY_BITS 28
 #define FX_DENSE_FIRST_BITS 14
@@ -1431,11 +1446,11 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
             int e;
             frexpf(v, &e);                               // v < 2^e
             int bits = FX_TARGET_BITS - e;
-            if (sc != 0.f && em != 0u) {                 // the largest entry stays < 2^28 units
+            if (em != 0u) {                              // the largest entry stays < 2^28 units
                 int ee;
-                frexpf((float)em / sc, &ee);
+                frexpf(__uint_as_float(em), &ee);
                 bits = min(bits, FX_ENTRY_BITS - ee);
-            } else if (!((hashed_mask >> l) & 1u)) {     // dense level, no entry measured yet
+            } else if (!((hashed_mask >> l) & 1u)) {     // dense level, no entry measured
                 bits = FX_DENSE_FIRST_BITS - e;
             }
             nx = scalbnf(1.0f, max(-126, min(126, bits)));
@@ -2061,7 +2076,7 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
     }
     hipStream_t st = (hipStream_t)stream;
     FxStats* stats = reinterpret_cast<FxStats*>(fx_vmax);
-    k_fx_esum<<<dim3(128, RN_L), 256, 0, st>>>(gm, fx_scale_cur, fx_acc, stats);
+    k_fx_esum<<<dim3(128, RN_L), 256, 0, st>>>(gm, fx_scale_cur, fx_acc, grid_grad, stats);
     k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo);
     RN_CHECK_LAUNCH();
     {   // every level (dense ones go fixed point from their second step)

@@ -42,11 +42,11 @@ def test_fx_matches_fp32_and_is_reproducible(cuda, B, K, scale):
     _, gfx1 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     n_fx = check_fx_vs_fp32(m, gfx1, g32, r, f"B{B} K{K} s{scale}")
     hashed, lv = _hashed(scale)
-    # every level: the hashed ones at the record scale, the dense ones (first
-    # fixed-point step) at the conservative first-step scale
+    # every level: the hashed ones at the record scale, the dense ones capped
+    # by their largest entry (read from the first step's fp32 gradient)
     assert n_fx == 16 and len(hashed) > 0
-    # from the next step on a dense level's scale is capped by its largest
-    # entry: steps 3 and 4 (identical inputs) use identical scales everywhere
+    # from the next step on the entry cap comes from the fixed-point entries:
+    # steps 3 and 4 (identical inputs) use identical scales everywhere
     _, gfx2 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     check_fx_vs_fp32(m, gfx2, g32, r, f"B{B} K{K} s{scale} step 3")
     _, gfx3 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
