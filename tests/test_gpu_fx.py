@@ -102,11 +102,12 @@ def test_fx_entry_wrap_sets_redo(cuda):
     """an int32 entry can wrap with every record under the 2^28-
     unit growth bound when many same-sign records land on it.  Here all 8192
     rays are the same ray (K = 2) with positive seeds: the coarse hashed
-    levels' entries take ~16k records each, and the step's scale is 4x the
-    one the previous identical step measured ("just under the 8x redo
-    threshold": no record reaches 2^28 units).  The level's exact
-    entry sum then differs from its record sum by a multiple of 2^32, the
-    redo flag is set, and the result is the fp32 one."""
+    levels' entries take ~16k records each.  The measured scale keeps the
+    largest entry under 2^28 units; the step runs at 16x that scale, so the
+    entries pass 2^31 while every record (~2^-14 of its entry) stays far
+    below the 2^28-unit growth bound (the vmax check does not fire).  The
+    level's exact entry sum then differs from its record sum by a multiple of
+    2^32, the redo flag is set, and the result is the fp32 one."""
     B, K = 8192, 2
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
     o = np.repeat(o[:1], B, 0)
@@ -117,10 +118,10 @@ def test_fx_entry_wrap_sets_redo(cuda):
     acc, scales, stats, redo = r.ws._fx
     cur = scales[r.ws.fx_i]
     hashed, lv = _hashed(0.5)
-    # the scale the previous step measured maps the largest record to
-    # [2^22, 2^23) units; 4x that keeps every record under 2^25 units, below
-    # the 2^28-unit growth bound (the vmax check does not fire)
-    f = 4.0
+    # the measured scale maps the largest entry below 2^28 units; 16x pushes
+    # the entries past 2^31 while the records (each a small part of its
+    # entry) stay far below the 2^28-unit growth bound
+    f = 16.0
     g_e = g32[0].view(-1, 2)
     units = {l: float(_level(g_e, lv, l).abs().max()) * float(cur[l]) * f for l in hashed}
     # the test's premise: some entry's exact integer sum exceeds the int32 range
