@@ -504,11 +504,13 @@ def main():
     if atom_req:
         # requests per launch from the PMC pass (tools/pmc_traffic.py), scaled to
         # this run's sample count; rate against the chip-wide atomic ceiling of
-        # this launch's mix: the dense levels' f32 adds and (fixed point) the
-        # hashed levels' u32 adds, weighted by their share of the requests
+        # this launch's mix of f32 adds and (fixed point) u32 adds
         req = atom_req * samples_per_step_rank / pmc_samples
         rate = req / (bwd_ms * 1e-3) / 1e9
-        u32_share = tj.get("u32_request_share", 0.0) if r.grid_fx and not args.split_bwd else 0.0
+        # fixed point: every level's records go in as u32 adds from the second
+        # step of a workspace on (round 3; round 2 kept the dense levels' 8 %
+        # of C3's requests in fp32)
+        u32_share = 1.0 if r.grid_fx and not args.split_bwd else 0.0
         peak = 1.0 / ((1 - u32_share) / ATOMIC_PEAK_GREQ + u32_share / ATOMIC_U32_PEAK_GREQ)
         roofline["atomic"] = {"requests_per_launch": round(req), "requests_per_sample":
                               round(req / samples_per_step_rank, 2),
