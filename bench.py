@@ -106,6 +106,9 @@ def parse():
     ap.add_argument("--split-bwd", action="store_true",
                     help="backward with one model per block (rn_field_bwd) instead of the "
                          "merged per-ray grid scatter (rn_field_bwd_merged)")
+    ap.add_argument("--grid-fx", type=int, default=None,
+                    help="fixed-point grid-gradient accumulation: 1 on, 0 fp32 atomics "
+                         "(default: the renderer's choice)")
     ap.add_argument("--max-chunk", type=int, default=None,
                     help="merged backward: largest chunk of merged samples per queue grab "
                          "(default: the renderer's, by rays x sub-NeRFs)")
@@ -236,6 +239,8 @@ def main():
     else:
         r = FusedMLRenderer(model, gate, B)
     r.merged_bwd = r.merged_bwd and not args.split_bwd
+    if args.grid_fx is not None:
+        r.grid_fx = bool(args.grid_fx)
     if args.max_chunk:
         r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk

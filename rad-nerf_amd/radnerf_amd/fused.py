@@ -183,8 +183,13 @@ class FusedMLRenderer:
         # adds, scale from the previous step's largest record, fp32 redo on
         # overflow; rn_grid_fx_fold): field_bwd C3 3.76 -> 3.50 ms, C4 per
         # GPU 3.29 -> 2.60, C5 10.54 -> 8.59 (tools/ablate.py, r02).  The
-        # first backward of a workspace runs fp32 (no scale yet).
-        self.grid_fx = True
+        # first backward of a workspace runs fp32 (no scale yet).  Its
+        # bookkeeping (entry sums, check, fold over the whole table: 0.06 ms,
+        # + 0.011 ms for the redo launch) is per step, not per sample: at C1's
+        # 1024 rays x 1 sub-NeRF fp32 atomics win (494 vs 462 M samples/s),
+        # from C2's 8192 rays on fixed point does (C2 800 vs 696, C3 1078 vs
+        # 998; tools/gpu/fx_small.sh, profiles/r03/fx_small_r03.jsonl)
+        self.grid_fx = rk > 1024
         self.min_chunk = 512
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)

@@ -85,6 +85,7 @@ def test_fx_nonfinite_seed_propagates(cuda):
     B, K = 512, 2
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
     r = get_renderer(m, g, B)
+    r.grid_fx = True                 # (512 rays x 2: fp32 by the renderer's own choice)
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)      # fp32 step: scales
     bad = [s.copy() for s in seeds]
     bad[0][7] = np.inf

@@ -120,6 +120,9 @@ def check_used_vs_oracle(w, ores, thr=1e-4):
 def test_fused_vs_dropin_vs_oracle(cuda, scale, K, B):
     esf = 1 / 256 if scale > 0.5 else 0.0
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, scale=scale, K=K)
+    # fixed point is the renderer's choice above 1024 rays x sub-NeRFs; these
+    # oracle-sized batches check it too
+    get_renderer(m, g, len(o)).grid_fx = True
     # the first fused backward accumulates the grid gradient in fp32 and
     # measures the records; the second runs the hashed levels in fixed point
     # (rn_grid_fx_fold): the one checked against the oracle below
