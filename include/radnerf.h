@@ -23,6 +23,9 @@ int rn_version(void);
 const char* rn_last_error(void);
 /* ablation switches for kernel studies (tools/ablate.py); 0 = production */
 void rn_set_debug_flags(int flags);
+/* ablation builds (debug flag 4096): per-phase wave cycles of the merged
+ * backward, summed over waves, read and cleared (synchronous) */
+int rn_debug_cycles(unsigned long long* out);
 
 /* ---- ray / AABB -----------------------------------------------------------
  * replaces vren.ray_aabb_intersect  (models/csrc/binding.cpp:4-16,

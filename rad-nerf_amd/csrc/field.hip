@@ -31,6 +31,11 @@
 #pragma clang fp contract(off)
 
 static int g_field_dbg = 0;
+// ablation builds only (flag 4096): per-phase wave cycles of the merged
+// backward, summed over waves (s_memtime): [0] MLP phase, [1] walk staging
+// (row loads + LDS fill, up to the barrier), [2] walks, [3] chunk tails
+// (walk2_end: flush + drain)
+__device__ unsigned long long g_rn_cyc[8];
 
 namespace {
 
@@ -511,9 +516,10 @@ __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& 
     return lv_const(sT, a.gm, l);
 }
 
-// walk one window: eighth e's samples are rows [32e, 32e + ne) of sG/sU
-// (ne per lane: its eighth's count; n0 = the largest, wave-uniform)
-template <int GM>
+// walk one window: the lane's eighth's samples are rows [0, ne) of its
+// eighth's staging block sG/sU (per-lane bases; ne per lane: its eighth's
+// count; n0 = the largest, wave-uniform; at most WIN)
+template <int GM, int WIN = 32>
 __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT,
                                              const float* sG_, const float* sU_, int ne, int n0,
                                              __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
@@ -526,7 +532,9 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
     const LvConst lc = walk2_level(a, sT);
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
     lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - wid) : wid);
-    const int s_base = eighth * 32;
+    // sG / sU are this lane's eighth's own block of WIN rows (per-lane bases)
+    const int s_base = 0;
+    (void)eighth;
     typedef float vf4 __attribute__((ext_vector_type(4)));
     typedef float vf2 __attribute__((ext_vector_type(2)));
     typedef __attribute__((address_space(3))) const vf4 lds_cf4;
@@ -684,7 +692,7 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
                                              rn_half* imgX, FwdState& st, bool valid, int64_t s,
                                              int wid, f32x16& accA, f32x16& accB,
                                              DwScale& cur, bool do_dw, float& gscale_out,
-                                             bool& zero_iter_out) {
+                                             bool& zero_iter_out, bool sync = true) {
     const int lane = rn_lane(), h = lane >> 5;
     const half8 z8 = rn_zero8();
     // ---- seeds (lanes h == 0 own the output rows)
@@ -706,7 +714,7 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         mg = fmaxf(mg, __shfl_xor(mg, off));
     }
     if (lane == 0) { sMax[2 * wid] = mr; sMax[2 * wid + 1] = mg; }
-    __syncthreads();                                                    // B0
+    if (sync) __syncthreads();                                                    // B0
     float bmr = sMax[0], bmg = sMax[1];
 #pragma unroll
     for (int w = 1; w < BWD_WAVES; ++w) { bmr = fmaxf(bmr, sMax[2 * w]); bmg = fmaxf(bmg, sMax[2 * w + 1]); }
@@ -738,7 +746,7 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
 #pragma unroll
         for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.r2[q]);
     }
-    __syncthreads();                                                    // B1
+    if (sync) __syncthreads();                                                    // B1
     if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
     half8 dr2f[4];
     {
@@ -748,13 +756,13 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         rn_acc_to_frags_masked(b0, st.r2[0], st.r2[1], dr2f[0], dr2f[1]);
         rn_acc_to_frags_masked(b1, st.r2[2], st.r2[3], dr2f[2], dr2f[3]);
     }
-    __syncthreads();                                                    // B2
+    if (sync) __syncthreads();                                                    // B2
     // ---- layer rgb2: dW (w2..w5) = dR2 x R1 ; dR1 = Wr2^T dR2 masked
     if (do_dw) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) { rn_img_write(imgY, q, dr2f[q]); rn_img_write(imgX, q, st.r1[q]); }
     }
-    __syncthreads();                                                    // B3
+    if (sync) __syncthreads();                                                    // B3
     if (do_dw && wid >= 2 && wid < 6)
         accA = dw_block_tile(sImg, 32 * ((wid - 2) >> 1), 32 * ((wid - 2) & 1), accA);
     half8 dr1f[4];
@@ -768,14 +776,14 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         rn_acc_to_frags_masked(b0, st.r1[0], st.r1[1], dr1f[0], dr1f[1]);
         rn_acc_to_frags_masked(b1, st.r1[2], st.r1[3], dr1f[2], dr1f[3]);
     }
-    __syncthreads();                                                    // B4
+    if (sync) __syncthreads();                                                    // B4
     // ---- layer rgb1: dW (w6, w7) = dR1 x [SH | geo 1..16] ; dG
     if (do_dw) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dr1f[q]);
         rn_img_write(imgX, 0, st.sh); rn_img_write(imgX, 1, st.gin);
     }
-    __syncthreads();                                                    // B5
+    if (sync) __syncthreads();                                                    // B5
     if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
     half8 dg0, dg1;
     {
@@ -786,14 +794,14 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         if (h == 0) b[8] = gsig * gscale;          // row 16 = dL/dh0
         rn_acc_to_frags<false>(b, dg0, dg1);
     }
-    __syncthreads();                                                    // B6
+    if (sync) __syncthreads();                                                    // B6
     // ---- layer geo2: dW (w0, w1) = dG x H1 ; dH1 = Wg2^T dG masked
     if (do_dw) {
         rn_img_write(imgY, 0, dg0); rn_img_write(imgY, 1, dg1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h1[q]);
     }
-    __syncthreads();                                                    // B7
+    if (sync) __syncthreads();                                                    // B7
     if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
     half8 dh1f[4];
     {
@@ -803,19 +811,19 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         rn_acc_to_frags_masked(b0, st.h1[0], st.h1[1], dh1f[0], dh1f[1]);
         rn_acc_to_frags_masked(b1, st.h1[2], st.h1[3], dh1f[2], dh1f[3]);
     }
-    __syncthreads();                                                    // B8
+    if (sync) __syncthreads();                                                    // B8
     // ---- layer geo1: dW (w2, w3) = dH1 x E ; dE = Wg1^T dH1
     if (do_dw) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) rn_img_write(imgY, q, dh1f[q]);
         rn_img_write(imgX, 0, st.e0); rn_img_write(imgX, 1, st.e1);
     }
-    __syncthreads();                                                    // B9
+    if (sync) __syncthreads();                                                    // B9
     if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
     f32x16 dE = rn_zero16();
 #pragma unroll
     for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
-    __syncthreads();                                                    // B10
+    if (sync) __syncthreads();                                                    // B10
     gscale_out = gscale;
     zero_iter_out = zero_iter;
     return dE;
@@ -922,6 +930,7 @@ k_field_bwd(FieldArgs a) {
 // ux uy uz | 1 / scale (fp32).  Half the 144 B of fp32 rows: the chunk's rows
 // stay in L2 for longer chunks.
 #define MB_ROW 20
+#define MB_WIN 64          // walk window: staged rows per chunk eighth
 #define CH_DESC 20         // chunk descriptor ints (80 B, 16-B aligned)
 #define MB_KMAX 8
 
@@ -965,6 +974,10 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         G.carry = rn_rsrc(G.carry_ptr, G.bytes);
     }
     if (GM == 2) G.fx = rn_rsrc(F.acc, 2 * a.grid_bytes);
+    // the walk phase stages its windows over the waves' images AND the
+    // weights (the weights are reloaded for the next chunk's MLP phase):
+    // eighths 0-3 in sImg (then the rings of waves 4-7), eighths 4-7 in sW.
+    // (One array for both made the compiler spill 80 VGPRs.)
     __shared__ __attribute__((aligned(16))) rn_half sW[FIELD_FRAGS * RN_FRAG_HALFS];
     __shared__ __attribute__((aligned(16))) rn_half sImg[BWD_WAVES * 2 * RN_IMG_HALFS];
     __shared__ float sMax[2 * BWD_WAVES];
@@ -993,20 +1006,34 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
     }
     const bool do_sc = !(dbg & 4);
-    float* sG = reinterpret_cast<float*>(sImg);
-    float* sU = sG + BWD_WAVES * 32 * SG_STRIDE;
-    // walk rings: waves 0-3 in sRing, waves 4-7 in the image region past the
-    // scatter staging (free during the scatter phase; drained every chunk)
+    // walk windows of MB_WIN rows per eighth: each window's staging loads
+    // wait (vmcnt, in issue order) for the atomics the previous window issued,
+    // so fewer, longer windows wait less often (round 3: 32 -> 64)
+    // one eighth's staging block: MB_WIN rows of dL/dE (SG_STRIDE floats)
+    // then MB_WIN unit coords + 1/scale (4 floats)
+    constexpr int EB = MB_WIN * (SG_STRIDE + 4);         // floats per eighth
+    auto eighth_g = [&](int e) -> float* {
+        return e < 4 ? reinterpret_cast<float*>(sImg) + e * EB
+                     : reinterpret_cast<float*>(sW) + (e - 4) * EB;
+    };
+    // walk rings: waves 0-3 in sRing, waves 4-7 in sImg past eighths 0-3
+    // (free during the scatter phase; drained every chunk)
     static_assert(4 * W2_RING_WORDS * 4 <= BWD_WAVES * SC_STREAMS * 3 * SC_RING * 4, "rings");
-    static_assert(BWD_WAVES * 32 * (SG_STRIDE + 4) * 4 + 4 * W2_RING_WORDS * 4 <=
-                  BWD_WAVES * 2 * RN_IMG_HALFS * 2, "rings in the image region");
+    static_assert(4 * EB * 4 + 4 * W2_RING_WORDS * 4 <= BWD_WAVES * 2 * RN_IMG_HALFS * 2,
+                  "eighths 0-3 + rings in the image region");
+    static_assert(4 * EB * 4 <= FIELD_FRAGS * RN_FRAG_HALFS * 2, "eighths 4-7 in the weights");
     uint32_t* ring2 = wid < 4 ? sRing + wid * W2_RING_WORDS
-                              : reinterpret_cast<uint32_t*>(sU + BWD_WAVES * 32 * 4) +
+                              : reinterpret_cast<uint32_t*>(sImg) + 4 * EB +
                                     (wid - 4) * W2_RING_WORDS;
+    // this lane's walk eighth (stream = lane >> 2, eighth = stream >> 1)
+    float* const wG = eighth_g(rn_lane() >> 3);
+    float* const wU = wG + MB_WIN * SG_STRIDE;
+    bool sw_ok = false;                          // sW holds model cur_k's weights
 
     f32x16 accA = rn_zero16(), accB = rn_zero16();
     DwScale cur = {0.f, 0.f};
     int cur_k = -1;
+    uint64_t cyc[4] = {0, 0, 0, 0};
     float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
     float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
     int n_local = 0;
@@ -1044,6 +1071,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         ++n_local;
 
         // ---- 1. MLP backward per model, rows staged in the block's scratch
+        const bool prof = ABL && (dbg & 4096);
+        uint64_t tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         for (int kk = 0; kk < K; ++kk) {
             const int k = rev ? K - 1 - kk : kk;
             const int a_k = sCh[2 + k], n_k = sCh[2 + MB_KMAX + k], roff = sCh[2 + 2 * MB_KMAX + k];
@@ -1062,7 +1091,13 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                     dw_unpark(park + (size_t)k * BWD_WAVES * 2048, accA, accB);
                 else { accA = rn_zero16(); accB = rn_zero16(); }
                 cur_k = k;
+            } else if (!sw_ok) {                 // the walk staged its rows over sW
+                __syncthreads();
+                rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
+                                FIELD_FRAGS * RN_FRAG_BYTES);
+                __syncthreads();
             }
+            sw_ok = true;
             for (int w0 = 0; w0 < n_k; w0 += BWD_WAVES * 32) {
                 rn_lds_order();
                 const int i = w0 + wid * 32 + c;
@@ -1076,8 +1111,11 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                                          CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, st,
                                          ux, uy, uz);
                 float gscale; bool zero_iter;
+                // ablation 512: no block barriers in the MLP phase (wrong
+                // results; timing of the barrier cost only)
                 const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid,
-                                             accA, accB, cur, do_dw, gscale, zero_iter);
+                                             accA, accB, cur, do_dw, gscale, zero_iter,
+                                             !(dbg & 512));
                 if (valid) {
                     const float ginv = zero_iter ? 0.f : 1.0f / gscale;
                     float* row = rows + (size_t)(roff + i) * MB_ROW;
@@ -1091,6 +1129,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 }
             }
         }
+        if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[0] += t - tp0; tp0 = t; }
         if (!do_sc) continue;
 
         // ---- 2. scatter in merged (ray, t) order
@@ -1105,11 +1144,18 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         Walk2 W;
         walk2_begin(W, ring2);
         W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB; W.sqA = sqA; W.sqB = sqB;
-        for (int w0 = 0; w0 < E; w0 += 32) {
-            const int j = threadIdx.x >> 1, half = threadIdx.x & 1;
-            const int e = j >> 5, jj = j & 31;
+        sw_ok = false;                           // the staging overwrites sW
+        for (int w0 = 0; w0 < E; w0 += MB_WIN) {
+          int nz = 0;
+#pragma unroll 1
+          for (int pass = 0; pass < MB_WIN / 32; ++pass) {
+            // wave e stages eighth e's rows [w0, w0 + MB_WIN), 32 per pass
+            const int half = threadIdx.x & 1;
+            const int e = wid, jj = pass * 32 + ((threadIdx.x >> 1) & 31);
+            float* const sG = eighth_g(e);               // wave-uniform
+            float* const sU = sG + MB_WIN * SG_STRIDE;
+            const int j = jj;                            // row of the eighth's block
             const int elen = max(0, min(E, n_p - e * E));
-            int nz = 0;
             if (w0 + jj < elen) {
                 const int smp = m.perm[p_base + e * E + w0 + jj];
                 int k = 0;
@@ -1134,19 +1180,28 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 }
                 if (half) *reinterpret_cast<nf4*>(sU + j * 4) = u;
             }
+          }
             // a window whose rows are all zero (rays past early termination)
             // adds nothing; skipping it keeps the walk state valid (entries
             // are identified by their coordinates)
-            if (__syncthreads_or(nz) && !(dbg & 32)) {
-                const int ne = max(0, min(32, elen_lane - w0));
-                const int n0 = max(0, min(32, min(E, n_p) - w0));
-                walk2_window<GM>(a, sT, sG, sU, ne, n0, grad_rs, G, W, dbg);
+            const bool live_w = __syncthreads_or(nz);
+            if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[1] += t - tp0; tp0 = t; }
+            if (live_w && !(dbg & 32)) {
+                const int ne = max(0, min(MB_WIN, elen_lane - w0));
+                const int n0 = max(0, min(MB_WIN, min(E, n_p) - w0));
+                walk2_window<GM, MB_WIN>(a, sT, wG, wU, ne, n0, grad_rs, G, W, dbg);
             }
             __syncthreads();
+            if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[2] += t - tp0; tp0 = t; }
         }
         walk2_end<GM>(a, sT, grad_rs, G, W, dbg);
+        if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[3] += t - tp0; tp0 = t; }
         vmA = W.vmA; vmB = W.vmB; sqA = W.sqA; sqB = W.sqB;
         __syncthreads();                         // rings (image region) drained
+    }
+    if (ABL && (dbg & 4096) && rn_lane() == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
     }
     if (GM == 2) {                               // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
@@ -1798,6 +1853,17 @@ extern "C" {
 
 void rn_set_debug_flags(int flags) { g_field_dbg = flags; }
 
+/* ablation builds: read and clear the per-phase cycle counters (8 x u64) */
+int rn_debug_cycles(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rn_cyc), sizeof(unsigned long long) * 8, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return 2;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_rn_cyc), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return 2;
+    return 0;
+}
+
 int rn_pack_f16(const float* src, int64_t src_stride, const int32_t* index, int64_t n,
                 int32_t n_models, int64_t dst_stride, void* dst, void* stream) {
     RN_CHECK_ARG(n >= 0 && n_models >= 1, "bad sizes");
@@ -1974,7 +2040,9 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         F.qsum = reinterpret_cast<FxStats*>(fx_vmax)->qsum;
     }
     const dim3 blk(BWD_WAVES * 64);
-    if (fx_mode == 2) {
+    if (fx_mode == 2 && a.dbg) {
+        k_field_bwd_merged<CACHE_READ, true, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (fx_mode == 2) {
         k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (fx_mode == 3) {
         k_field_bwd_merged<CACHE_READ, false, 3><<<blocks, blk, 0, st>>>(a, m, G, F);

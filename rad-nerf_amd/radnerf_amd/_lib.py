@@ -28,6 +28,7 @@ SIGNATURES = {
     "rn_field_dinput": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                         P, I32, P],
     "rn_field_density": [P, I64, P, P, P, P, P, P, P, P, P, P, P],
+    "rn_debug_cycles": [P],
     "rn_density_update_sampled": [P, P, I32, I32, I32, F32, F32, F32, U64, P, P, P, P, P, P, P,
                                   P, P, P, P, P, P, P],
     "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],

@@ -7,6 +7,7 @@ _field call includes rn_grid_fx_fold and the redo launch), "x" = merged
 backward with fp32 grid atomics, "s" = per-model backward, "i" = merged
 backward with integer accumulation, "f" = field_fwd.
 Workload from ABL_K / ABL_SCALE / ABL_RAYS (default C3)."""
+import ctypes
 import json
 import os
 import sys
@@ -51,6 +52,7 @@ def main():
     # tokens: "<flags>" = field_bwd (merged) with debug flags, "s<flags>" = the
     # per-model field_bwd, "f<flags>" = field_fwd
     times = {f: [] for f in flags}
+    phases = {}
     fwd = []
     for rnd in range(5):
         for f in flags:
@@ -67,6 +69,10 @@ def main():
             b.record()
             torch.cuda.synchronize()
             times[f].append(a.elapsed_time(b))
+            if int(f.lstrip("fsix")) & 4096:
+                cyc = (ctypes.c_ulonglong * 8)()
+                L.debug_cycles(ctypes.cast(cyc, ctypes.c_void_p).value)
+                phases.setdefault(f, []).append([int(c) for c in cyc[:4]])
         L.set_debug_flags(0)
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
@@ -78,7 +84,13 @@ def main():
            "field_bwd_ms": {str(f): float(np.median(v)) for f, v in times.items()
                             if not f.startswith("f")},
            "field_fwd_flags_ms": {str(f): float(np.median(v)) for f, v in times.items()
-                                  if f.startswith("f")}}
+                                  if f.startswith("f")},
+           # flag 4096: summed wave cycles per phase (MLP, staging, walk, chunk
+           # tails), median over rounds, as fractions of their sum
+           "phases": {f: dict(zip(("mlp", "staging", "walk", "tail"),
+                                  [round(float(x), 4) for x in
+                                   (np.median(np.array(v), 0) / np.median(np.array(v), 0).sum())]))
+                      for f, v in phases.items()}}
     print(json.dumps(out))
 
 
