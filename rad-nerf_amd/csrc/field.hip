@@ -1069,6 +1069,16 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         if (r0 >= B) break;
         const bool rev = n_local & 1;
         ++n_local;
+        // the chunk's rays into LDS (the walk rings' area, free until the
+        // walk): the MLP tiles look a sample's ray up there
+        constexpr int RAYS_LDS = BWD_WAVES * SC_STREAMS * 3 * SC_RING / 6;
+        const int nr_lds = r1 - r0 <= RAYS_LDS ? r1 - r0 : 0;
+        float* sRays = reinterpret_cast<float*>(sRing);
+        for (int i = threadIdx.x; i < 6 * nr_lds; i += blockDim.x) {
+            const int q = i / 6, cc = i - 6 * q;
+            sRays[i] = cc < 3 ? a.rays_o[3 * (r0 + q) + cc] : a.rays_d[3 * (r0 + q) + cc - 3];
+        }
+        __syncthreads();
 
         // ---- 1. MLP backward per model, rows staged in the block's scratch
         const bool prof = ABL && (dbg & 4096);
@@ -1107,9 +1117,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 const int64_t s = a_k + (valid ? ((dbg & 256) ? (i & 31) : i) : 0);
                 FwdState st;
                 float ux, uy, uz;
-                tile_forward_s<1, CACHE>(a, sT, sW, s, valid,
-                                         CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, st,
-                                         ux, uy, uz);
+                tile_forward_rays<CACHE>(a, sT, sW, s, valid,
+                                         CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, sRays,
+                                         r0, nr_lds, st, ux, uy, uz);
                 float gscale; bool zero_iter;
                 // ablation 512: no block barriers in the MLP phase (wrong
                 // results; timing of the barrier cost only)
