@@ -360,3 +360,24 @@ def test_fused_outputs_without_gradient_raise(cuda):
     with pytest.raises(RuntimeError, match="reused"):
         _ = r1["ts"]
     assert r2["ts"].numel() == int(r2["rm_samples"])
+
+
+def test_ngp_sampled_density_update_through_dist(cuda):
+    """radnerf_amd.dist.update_density_grid on a single NGP with
+    warmup=False passes the step's seed through NGP.update_density_grid
+    (its override once dropped the keyword: TypeError) to the device-side
+    sampled update; the same (seed, step) gives the same grid and bitfield."""
+    from radnerf_amd import dist as rdist
+    m, _, _, _ = _ngp_setup(cuda, 64)
+    thr = 0.01 * 1024 / 3 ** 0.5
+    rdist.update_density_grid(m, thr, 0, warmup=True)
+    g0 = m.density_grid.clone()
+    outs = []
+    for _ in range(2):
+        with torch.no_grad():
+            m.density_grid_0.copy_(g0)
+        rdist.update_density_grid(m, thr, 5, warmup=False, seed=3)
+        torch.cuda.synchronize()
+        outs.append((m.density_grid.clone(), m.density_bitfield.clone()))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert not torch.equal(outs[0][0], g0)
