@@ -1074,7 +1074,10 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         constexpr int RAYS_LDS = BWD_WAVES * SC_STREAMS * 3 * SC_RING / 6;
         const int nr_lds = r1 - r0 <= RAYS_LDS ? r1 - r0 : 0;
         float* sRays = reinterpret_cast<float*>(sRing);
-        stage_rays(a, sRays, r0, nr_lds);
+        for (int i = threadIdx.x; i < 6 * nr_lds; i += blockDim.x) {
+            const int q = i / 6, cc = i - 6 * q;
+            sRays[i] = cc < 3 ? a.rays_o[3 * (r0 + q) + cc] : a.rays_d[3 * (r0 + q) + cc - 3];
+        }
         __syncthreads();
 
         // ---- 1. MLP backward per model, rows staged in the block's scratch
@@ -1253,7 +1256,6 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
 // ---------------------------------------------------------------------------
 #define FM_KMAX 8
 #define FM_LDS_K 4
-#define FM_RAYS 1024       // rays per chunk staged in LDS
 
 template <int CACHE, bool ENC_M, bool GW>
 __global__ void __launch_bounds__(1024)
@@ -1261,10 +1263,6 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
     __shared__ LvTab sT;
     __shared__ int32_t sCh[2][2 + 2 * FM_KMAX];      // this and the previous chunk
-    // the rays of this and the previous chunk (a sample's ray from LDS, not a
-    // second dependent global load); a chunk with more rays reads them from
-    // global memory
-    __shared__ float sRaysF[2][FM_RAYS * 6];
     const int K = m.n_models, B = m.n_rays;
     if (!GW) {
         for (int k = 0; k < K; ++k)
@@ -1281,7 +1279,7 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
 
     // per-model MLP tile u of chunk descriptor ch (tile i of model 0, tile i
     // of model 1, ...); false: past the end
-    auto mlp_tile = [&](const int32_t* ch, const float* sR, int u) {
+    auto mlp_tile = [&](const int32_t* ch, int u) {
         const int k = u % K, t = u / K;
         const int n_k = ch[2 + FM_KMAX + k];
         if (t * 32 >= n_k) return;                           // wave-uniform
@@ -1294,9 +1292,8 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
         constexpr int TC = ENC_M ? CACHE_READ_NT : CACHE;
         const rn_half* W = GW ? a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS
                               : sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS;
-        const int nr = ch[1] - ch[0] <= FM_RAYS ? ch[1] - ch[0] : 0;
-        tile_forward_rays<TC>(a, sT, W, s, valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
-                              sR, ch[0], nr, st, ux, uy, uz);
+        tile_forward_s<1, TC>(a, sT, W, s, valid, TC != CACHE_NONE ? cache_slot(a, s) : nullptr,
+                              st, ux, uy, uz);
         if (valid && h == 0) {
             a.sigma[s] = expf(st.g0);
             a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
@@ -1334,15 +1331,10 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
         }
         __syncthreads();
         const bool live = cur[0] < B;
-        float* const sRc = sRaysF[it & 1];
-        const float* const sRp = sRaysF[(it & 1) ^ 1];
-        const int nr_c = live && cur[1] - cur[0] <= FM_RAYS ? cur[1] - cur[0] : 0;
-        stage_rays(a, sRc, cur[0], nr_c);
-        __syncthreads();
         if (!ENC_M) {
             if (!live) break;
             const int nt = mlp_tiles(cur);
-            for (int u = wid; u < nt; u += waves) mlp_tile(cur, sRc, u);
+            for (int u = wid; u < nt; u += waves) mlp_tile(cur, u);
             continue;
         }
         // Merged-order encoding, software-pipelined over chunks: iteration it
@@ -1358,12 +1350,12 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
         const int nA = (n_p + 31) >> 5;
         const int nB = prev_live ? mlp_tiles(prev) : 0;
         for (int u = wid; u < nA + nB; u += waves) {
-            if (u >= nA) { mlp_tile(prev, sRp, u - nA); continue; }
+            if (u >= nA) { mlp_tile(prev, u - nA); continue; }
             const int q = u * 32 + c;
             const bool valid = q < n_p;
             const int64_t s = m.perm[p_base + (valid ? q : 0)];
             float x, y, z, dx, dy, dz;
-            load_sample_rays(a, s, sRc, cur[0], nr_c, x, y, z, dx, dy, dz);
+            load_sample<1>(a, s, x, y, z, dx, dy, dz);
             const float ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
             const float uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
             const float uz = unit_coord(z, a.xyz_min[2], a.extent[2]);

@@ -383,44 +383,29 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
 // origin, direction): the ray lookup of a sample is an LDS read instead of a
 // second dependent global load; rays outside the table (nr = 0: the chunk had
 // too many) come from global memory.  Same arithmetic as load_sample<1>.
-__device__ __forceinline__ void load_sample_rays(const FieldArgs& a, int64_t s,
-                                                 const float* sRays, int r0, int nr, float& x,
-                                                 float& y, float& z, float& dx, float& dy,
-                                                 float& dz) {
-    const int r = a.ray_of[s];
-    const float t = a.ts[s];
-    const uint32_t q = (uint32_t)(r - r0);
-    float ox, oy, oz;
-    if (q < (uint32_t)nr) {
-        typedef __attribute__((address_space(3))) const float lds_f;
-        lds_f* p = (lds_f*)sRays + 6 * q;
-        ox = p[0]; oy = p[1]; oz = p[2]; dx = p[3]; dy = p[4]; dz = p[5];
-    } else {
-        ox = a.rays_o[3 * r]; oy = a.rays_o[3 * r + 1]; oz = a.rays_o[3 * r + 2];
-        dx = a.rays_d[3 * r]; dy = a.rays_d[3 * r + 1]; dz = a.rays_d[3 * r + 2];
-    }
-    // bit-identical to load_sample<1> (and to the march's sample position)
-    x = fmaf(t, dx, ox);
-    y = fmaf(t, dy, oy);
-    z = fmaf(t, dz, oz);
-}
-
-// stage rays [r0, r0 + nr) (origin, direction: 6 floats each) into sRays;
-// the caller synchronises the block afterwards
-__device__ __forceinline__ void stage_rays(const FieldArgs& a, float* sRays, int r0, int nr) {
-    for (int i = threadIdx.x; i < 6 * nr; i += blockDim.x) {
-        const int q = i / 6, cc = i - 6 * q;
-        sRays[i] = cc < 3 ? a.rays_o[3 * (r0 + q) + cc] : a.rays_d[3 * (r0 + q) + cc - 3];
-    }
-}
-
 template <int CACHE>
 __device__ __forceinline__ void tile_forward_rays(const FieldArgs& a, const LvTab& T,
                                                   const rn_half* W, int64_t s, bool valid,
                                                   half8* fc, const float* sRays, int r0, int nr,
                                                   FwdState& st, float& ux, float& uy, float& uz) {
     float x = 0.f, y = 0.f, z = 0.f, dx = 1.f, dy = 0.f, dz = 0.f;
-    if (valid) load_sample_rays(a, s, sRays, r0, nr, x, y, z, dx, dy, dz);
+    if (valid) {
+        const int r = a.ray_of[s];
+        const float t = a.ts[s];
+        const uint32_t q = (uint32_t)(r - r0);
+        float ox, oy, oz;
+        if (q < (uint32_t)nr) {
+            typedef __attribute__((address_space(3))) const float lds_f;
+            lds_f* p = (lds_f*)sRays + 6 * q;
+            ox = p[0]; oy = p[1]; oz = p[2]; dx = p[3]; dy = p[4]; dz = p[5];
+        } else {
+            ox = a.rays_o[3 * r]; oy = a.rays_o[3 * r + 1]; oz = a.rays_o[3 * r + 2];
+            dx = a.rays_d[3 * r]; dy = a.rays_d[3 * r + 1]; dz = a.rays_d[3 * r + 2];
+        }
+        x = fmaf(t, dx, ox);
+        y = fmaf(t, dy, oy);
+        z = fmaf(t, dz, oz);
+    }
     tile_forward_pos<CACHE>(a, T, W, x, y, z, dx, dy, dz, valid, fc, st, ux, uy, uz);
 }
 
