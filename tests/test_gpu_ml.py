@@ -442,3 +442,28 @@ def test_input_grads_vs_oracle(cuda, scale, K, B):
         assert _rel(mg.cpu().numpy(), ores["mlp_grad"]) <= 4e-3
     assert rel(out["fused"][0], out["dropin"][0]) <= 1e-3
     assert rel(out["fused"][1], out["dropin"][1]) <= 1e-3
+
+
+@pytest.mark.parametrize("K", [2, 4])
+def test_fused_mostly_empty_rays(cuda, K):
+    """Chunks are cut by merged sample positions, so a chunk spans every ray
+    without samples between its first and last sample.  With 7 in 8 rays
+    pointed away from the box, chunks hold thousands of empty rays: more than
+    the merged backward stages in LDS (1,536), which then looks rays up in
+    global memory.  Fused chain vs the drop-in chain: outputs and gradients."""
+    B, scale = 8192, 0.5
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    o = o.copy()
+    d = d.copy()
+    away = np.arange(B) % 8 != 0
+    d[away] = -d[away]                    # origins sit outside the box, aimed at it
+    rf, gf = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
+    w = get_renderer(m, g, B).ws
+    cnt = w.counts.cpu().numpy().sum(0)
+    assert (cnt[away] == 0).mean() > 0.99 and (cnt[~away] > 0).mean() > 0.9
+    rd, gd = _run(ml_render, m, g, o, d, noise, seeds, cuda, 0.0)
+    for k in ("rgb", "opacity", "depth", "gating_code"):
+        assert torch.allclose(rf[k], rd[k], atol=1e-5, rtol=0), k
+    for a, b in zip(gf, gd):
+        rel = (a - b).norm() / b.norm().clamp_min(1e-30)
+        assert rel <= 1e-3, rel
