@@ -692,18 +692,22 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
                                              rn_half* imgX, FwdState& st, bool valid, int64_t s,
                                              int wid, f32x16& accA, f32x16& accB,
                                              DwScale& cur, bool do_dw, float& gscale_out,
-                                             bool& zero_iter_out, bool sync = true) {
+                                             bool& zero_iter_out, bool sync = true,
+                                             const float* pre = nullptr) {
     const int lane = rn_lane(), h = lane >> 5;
     const half8 z8 = rn_zero8();
-    // ---- seeds (lanes h == 0 own the output rows)
+    // ---- seeds (lanes h == 0 own the output rows); `pre`: dL/dsigma and
+    // dL/drgb already loaded by the caller (ahead of the forward recompute)
     float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
     if (valid && h == 0) {
-        const float ds = a.dsigma[s];
+        const float ds = pre ? pre[0] : a.dsigma[s];
+        const float r0 = pre ? pre[1] : a.drgb[3 * s], r1 = pre ? pre[2] : a.drgb[3 * s + 1],
+                    r2 = pre ? pre[3] : a.drgb[3 * s + 2];
         const float y0 = sigmoidf(st.out[0]), y1 = sigmoidf(st.out[1]),
                     y2 = sigmoidf(st.out[2]);
-        o0 = a.drgb[3 * s] * (y0 * (1.0f - y0));        // sigmoid'
-        o1 = a.drgb[3 * s + 1] * (y1 * (1.0f - y1));
-        o2 = a.drgb[3 * s + 2] * (y2 * (1.0f - y2));
+        o0 = r0 * (y0 * (1.0f - y0));                    // sigmoid'
+        o1 = r1 * (y1 * (1.0f - y1));
+        o2 = r2 * (y2 * (1.0f - y2));
         // TruncExp.backward: g * exp(clamp(x, -15, 15))  (custom_functions.py:171-173)
         gsig = ds * expf(fminf(fmaxf(st.g0, -15.f), 15.f));
     }
@@ -1117,6 +1121,13 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 const int64_t s = a_k + (valid ? ((dbg & 256) ? (i & 31) : i) : 0);
                 FwdState st;
                 float ux, uy, uz;
+                // the backward seeds, loaded ahead of the forward recompute
+                // (their latency hides behind its MFMAs)
+                float pre[4] = {0.f, 0.f, 0.f, 0.f};
+                if (valid && h == 0) {
+                    pre[0] = a.dsigma[s];
+                    pre[1] = a.drgb[3 * s]; pre[2] = a.drgb[3 * s + 1]; pre[3] = a.drgb[3 * s + 2];
+                }
                 tile_forward_rays<CACHE>(a, sT, sW, s, valid,
                                          CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, sRays,
                                          r0, nr_lds, st, ux, uy, uz);
@@ -1125,7 +1136,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 // results; timing of the barrier cost only)
                 const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid,
                                              accA, accB, cur, do_dw, gscale, zero_iter,
-                                             !(dbg & 512));
+                                             !(dbg & 512), pre);
                 if (valid) {
                     const float ginv = zero_iter ? 0.f : 1.0f / gscale;
                     float* row = rows + (size_t)(roff + i) * MB_ROW;
