@@ -595,11 +595,16 @@ class _GradNotSupported(torch.autograd.Function):
             "output; render with fused=False to differentiate it")
 
 
-def grad_unsupported(x, anchor, what):
-    """x as a graph output whose backward raises (see _GradNotSupported);
-    x itself (detached) when autograd is off or the anchor needs no grad."""
-    if torch.is_grad_enabled() and anchor.requires_grad:
-        return _GradNotSupported.apply(x, anchor, what)
+def grad_unsupported(x, anchors, what):
+    """x as a graph output whose backward raises (see _GradNotSupported),
+    anchored to the first of `anchors` (a tensor or a sequence of them) that
+    requires grad; x itself (detached) when autograd is off or none does."""
+    if torch.is_tensor(anchors):
+        anchors = (anchors,)
+    if torch.is_grad_enabled():
+        for anchor in anchors:
+            if anchor.requires_grad:
+                return _GradNotSupported.apply(x, anchor, what)
     return x
 
 
@@ -651,8 +656,9 @@ def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **k
     w = r.ws
     # each sub-NeRF's own colour (ml_rendering.py:65,73): values only -- a loss
     # on them raises at backward (the fused backward seeds the combined rgb)
+    anchors = (model.mlp_params, model.xyz_encoder.params, gating_net.params)
     singles = [grad_unsupported(w.rgb_k[i] + bg * (1 - w.opacity_k[i])[:, None],
-                                model.mlp_params, "ml_render independent_rgbs")
+                                anchors, "ml_render independent_rgbs")
                for i in range(K)]
     return {"rgb": rgb, "independent_rgbs": singles, "depth": depth, "opacity": opacity,
             "gating_code": gate, "gating_importance": gate.sum(0)}

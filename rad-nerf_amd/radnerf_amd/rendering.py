@@ -214,7 +214,8 @@ def _train_fused(model, rays_o, rays_d, kw):
     res = ml_render_fused(model, gate, rays_o, rays_d, rays_d, **kw)
     r = get_renderer(model, gate, rays_o.shape[0], grad=torch.is_grad_enabled())
     return _TrainResults({"rgb": res["rgb"], "opacity": res["opacity"],
-                          "depth": res["depth"][:, 0]}, r, model.mlp_params)
+                          "depth": res["depth"][:, 0]}, r,
+                         (model.mlp_params, model.xyz_encoder.params))
 
 
 def render(model, rays_o, rays_d, **kwargs):
@@ -237,6 +238,9 @@ def render(model, rays_o, rays_d, **kwargs):
 
 def _to_host(res, kw):
     if kw.get("to_cpu", False):
+        if isinstance(res, _TrainResults):
+            for k in _TrainResults.LAZY:         # materialise before copying out
+                res[k]
         res = {k: (v.cpu() if torch.is_tensor(v) else v) for k, v in res.items()}
         if kw.get("to_numpy", False):
             res = {k: (v.numpy() if torch.is_tensor(v) else v) for k, v in res.items()}
