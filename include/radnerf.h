@@ -316,6 +316,27 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
                         const int32_t* perm, int32_t blocks, int32_t threads, void* stream);
 
+/* Level-partitioned merged forward: the same sigma, rgb and feat_cache as
+ * rn_field_fwd_merged with the merged-order encoding (bit-exact), in three
+ * launches: the merged order's unit coordinates (prep: 16 B per merged
+ * sample), then the encoding split by level (block b encodes levels g and
+ * 15 - g, g = b % 8, of every sample into planes[L * plane_stride + s], one
+ * f16x2 per level; blocks go to the XCDs round-robin, so each XCD's L2 holds
+ * two levels' tables), then the per-model MLP tiles read the planes.
+ * plane_stride > every sample index; enc_blocks a multiple of 8; mlp_blocks of
+ * 1024 threads.  xq (optional, 64 int32): [8 g + x] = blocks of group g that
+ * ran on XCD x (a probe of the mapping).  Replaces the same reference path as
+ * rn_field_fwd_merged (models/networks.py:300-328 via ml_rendering.py:174-179). */
+int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        int64_t n_rays, int32_t n_models, const void* grid_f16,
+                        const uint32_t* level_offset, const uint32_t* level_hsize,
+                        const uint32_t* level_res, const float* level_scale,
+                        const float* xyz_min, const float* extent, const void* frags,
+                        float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
+                        const int32_t* perm, uint32_t* planes, int64_t plane_stride, void* prep,
+                        int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq, void* stream);
+
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------
  * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)
  * as (x, x+3, 6) or rays_o/rays_d as (rays_o, rays_d, 3).  importance (K) is

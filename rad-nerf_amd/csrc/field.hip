@@ -1379,6 +1379,117 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
 }
 
 
+// ---------------------------------------------------------------------------
+// Level-partitioned forward (round 3, after a probe: tools/enc_probe.py).
+// The merged forward gathers all sixteen levels of a sample on one CU, so
+// every XCD's 4 MB L2 faces the whole 23 MB table and the fine levels miss
+// it for nearly every sample (27 fabric requests per sample at C5).  Here
+// the encoding is split by level instead:
+//   1. k_enc_prep: per merged position p the sample's unit coordinates and
+//      index (16 B), computed once (bit-identical to load_sample<1>);
+//   2. k_field_encode_levels: block b encodes levels g and 15 - g, g = b % 8,
+//      for every sample.  Workgroups are dispatched to the XCDs round-robin
+//      (a rotation that varies by dispatch: measured, group g ran on XCD
+//      g - 1 for all its blocks), so each XCD gathers from two levels' tables
+//      only; correctness does not depend on the mapping.  Output: one f16x2
+//      plane per level, planes[L][s] (bit-identical to encode_lane);
+//   3. k_field_mlp_planes: the MLP tiles per model read the 8 levels of each
+//      lane from the planes, write sigma / rgb and the encoding cache (tile
+//      layout) that the backward and the input-gradient kernels read.
+// Static splits, no ticket queues (a per-XCD ticket word serialised at
+// ~100 ns per ticket: 1.9 ms at C3).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+k_enc_prep(FieldArgs a, MergeArgs m, float4* __restrict__ prep) {
+    const int P = m.mstart[m.n_rays];
+    for (int p = blockIdx.x * blockDim.x + threadIdx.x; p < P; p += gridDim.x * blockDim.x) {
+        const int s = m.perm[p];
+        float x, y, z, dx, dy, dz;
+        load_sample<1>(a, s, x, y, z, dx, dy, dz);
+        prep[p] = make_float4(unit_coord(x, a.xyz_min[0], a.extent[0]),
+                              unit_coord(y, a.xyz_min[1], a.extent[1]),
+                              unit_coord(z, a.xyz_min[2], a.extent[2]), __int_as_float(s));
+    }
+}
+
+__global__ void __launch_bounds__(256)
+k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
+                      int32_t* __restrict__ xq) {
+    __shared__ LvTab sT;
+    lv_stage(sT, a.gm);
+    __syncthreads();
+    const int g = blockIdx.x & 7;
+    if (xq && threadIdx.x == 0) {           // probe: group g's blocks per XCD
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+        atomicAdd(xq + 8 * g + (int)(xcc & 7u), 1);
+    }
+    const int la = g, lb = RN_L - 1 - g;
+    const int P = m.mstart[m.n_rays];
+    const int nt = (P + 31) >> 5;
+    const int nb = (int)(gridDim.x >> 3), j = (int)(blockIdx.x >> 3);
+    const int t0 = (int)((int64_t)nt * j / nb), t1 = (int)((int64_t)nt * (j + 1) / nb);
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), waves = blockDim.x >> 6;
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    const __amdgpu_buffer_rsrc_t rs = rn_rsrc(a.grid, a.grid_bytes);
+    uint32_t* const out = const_cast<uint32_t*>(a.planes) + (size_t)(h ? lb : la) * a.plane_stride;
+    for (int t = t0 + wid; t < t1; t += waves) {
+        const int p = t * 32 + c;
+        const bool valid = p < P;
+        const float4 q = prep[valid ? p : 0];
+        const uint32_t v = encode_pair(a, sT, rs, h, la, lb, q.x, q.y, q.z, valid);
+        if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
+    }
+}
+
+// MLP tiles of the K models (tile u: model k's 32 samples from seg_base[k] +
+// 32 t), waves strided over the flat tile list
+template <bool GW>
+__global__ void __launch_bounds__(1024)
+k_field_mlp_planes(FieldArgs a, int K) {
+    extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
+    __shared__ LvTab sT;
+    if (!GW) {
+        for (int k = 0; k < K; ++k)
+            rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
+                            a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
+                            FIELD_FWD_FRAGS * RN_FRAG_BYTES);
+    }
+    lv_stage(sT, a.gm);
+    __syncthreads();
+    int nt[FM_KMAX];
+    int total = 0;
+    for (int k = 0; k < K; ++k) {
+        nt[k] = (__builtin_amdgcn_readfirstlane(a.seg_count[k]) + 31) >> 5;
+        total += nt[k];
+    }
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int W = (int)(gridDim.x * (blockDim.x >> 6));
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    for (int u = (int)blockIdx.x * (int)(blockDim.x >> 6) + wid; u < total; u += W) {
+        int k = 0, t = u;
+        while (k < K - 1 && t >= nt[k]) { t -= nt[k]; ++k; }
+        const int n_k = a.seg_count[k];
+        const int i = t * 32 + c;
+        const bool valid = i < n_k;
+        const int64_t s = a.seg_base[k] + (valid ? i : 0);
+        FwdState st;
+        float ux, uy, uz;
+        const rn_half* Wk = GW ? a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS
+                               : sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS;
+        rn_lds_order();
+        tile_forward_s<1, CACHE_PLANES>(a, sT, Wk, s, valid, a.feat ? cache_slot(a, s) : nullptr,
+                                        st, ux, uy, uz);
+        if (valid && h == 0) {
+            a.sigma[s] = expf(st.g0);
+            a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
+            a.rgb[3 * s + 1] = sigmoidf(st.out[1]);
+            a.rgb[3 * s + 2] = sigmoidf(st.out[2]);
+        }
+    }
+}
+
+
 // Integer-mode scale: 2^(26 - e) with 2^(e-1) <= M < 2^e, M the largest
 // backward seed of the step (|dL/dsigma * sigma|, |dL/drgb|), so a seed-sized
 // contribution is ~2^26 units; larger ones carry exactly.
@@ -2125,6 +2236,53 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     else if (feat_cache) RN_FM_LAUNCH(CACHE_WRITE, false);
     else RN_FM_LAUNCH(CACHE_NONE, false);
 #undef RN_FM_LAUNCH
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+/* level-partitioned merged forward (k_enc_prep + k_field_encode_levels +
+   k_field_mlp_planes): the same outputs and encoding cache as
+   rn_field_fwd_merged with the merged-order encoding.  planes: 16 x
+   plane_stride u32 (plane_stride >= every sample index + 1); prep: 16 B per
+   merged sample; xq (optional probe): 64 int32, [8 g + x] += blocks of level
+   group g that ran on XCD x. */
+int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* rays_o,
+                        const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
+                        int64_t n_rays, int32_t n_models, const void* grid_f16,
+                        const uint32_t* level_offset, const uint32_t* level_hsize,
+                        const uint32_t* level_res, const float* level_scale,
+                        const float* xyz_min, const float* extent, const void* frags,
+                        float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
+                        const int32_t* perm, uint32_t* planes, int64_t plane_stride, void* prep,
+                        int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq, void* stream) {
+    RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && plane_stride >= 1,
+                 "bad sizes (n_models <= 8)");
+    RN_CHECK_ARG(enc_blocks >= 8 && enc_blocks % 8 == 0 && mlp_blocks >= 1,
+                 "bad launch (enc_blocks: a multiple of 8)");
+    RN_CHECK_ARG(ts && ray_of && rays_o && rays_d && seg_base && seg_count && grid_f16 &&
+                 level_offset && level_hsize && level_res && level_scale && xyz_min && extent &&
+                 frags && sigma && rgb && mstart && perm && planes && prep, "null pointer");
+    FieldArgs a{};
+    fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
+    a.dbg = g_field_dbg;
+    a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
+    a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
+    a.planes = planes; a.plane_stride = plane_stride;
+    a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
+    a.seg_base = seg_base; a.seg_count = seg_count;
+    MergeArgs m{};
+    m.mstart = mstart; m.perm = perm; m.n_rays = (int)n_rays; m.n_models = n_models;
+    hipStream_t st = (hipStream_t)stream;
+    if (xq && hipMemsetAsync(xq, 0, 64 * sizeof(int32_t), st) != hipSuccess) {
+        rn_set_error("%s: probe reset failed", __func__);
+        return 2;
+    }
+    k_enc_prep<<<1024, 256, 0, st>>>(a, m, (float4*)prep);
+    k_field_encode_levels<<<enc_blocks, 256, 0, st>>>(a, m, (const float4*)prep, xq);
+    const bool gw = n_models > FM_LDS_K;
+    if (gw) k_field_mlp_planes<true><<<mlp_blocks, 1024, 0, st>>>(a, n_models);
+    else k_field_mlp_planes<false><<<mlp_blocks, 1024,
+                                     (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES, st>>>(a, n_models);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -37,6 +37,8 @@ struct FieldArgs {
     float* sigma; float* rgb; // forward outputs
     const float* dsigma; const float* drgb;               // backward seeds
     rn_half* feat;            // optional encoding cache: [sample tiles][64 lanes][16] f16
+    const uint32_t* planes;   // level-partitioned encoding: [16 levels][plane_stride] f16x2
+    int64_t plane_stride;
     float xyz_min[3]; float extent[3];
     uint32_t grid_bytes;      // byte size of the f16 table (= of the f32 grad / 2)
     int dbg;                  // ablation flags (rn_set_debug_flags), 0 in production
@@ -275,6 +277,91 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
     for (int j = 0; j < 8; ++j) { e0[j] = (rn_half)f[j]; e1[j] = (rn_half)f[8 + j]; }
 }
 
+// Two levels of the tile's 32 samples, the same arithmetic as encode_lane
+// (bit-identical features): wave half 0 computes level la's cell position
+// and row hashes, half 1 level lb's, v_permlane32_swap hands them across,
+// every lane gathers the 4 rows of its x-half for both levels, and the
+// x-halves are summed with a second swap.  Returns the features of level
+// (h ? lb : la) as packed f16x2 (feature 0 low).  la, lb wave-uniform.
+__device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, const LvTab& T,
+                                                __amdgpu_buffer_rsrc_t rs, int h, int la, int lb,
+                                                float ux, float uy, float uz, bool valid) {
+    uint32_t GX[2], ROW[2][4];
+    float FX[2], FY[2], FZ[2];
+    {
+        const LvConst lm = lv_const(T, a.gm, h ? lb : la);
+        const LevelPos p = level_pos(lm.sc, ux, uy, uz);
+        uint32_t rw[4];
+        if (lm.dense) {
+            const uint32_t b = __umul24(p.gy, lm.res) + __umul24(p.gz, lm.res2);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                rw[r] = b + ((r & 1) ? lm.res : 0u) + ((r >> 1) ? lm.res2 : 0u);
+        } else {
+            const uint32_t y0 = p.gy * 2654435761u, z0 = p.gz * 805459861u;
+            const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rw[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
+        }
+        auto xch = [&](uint32_t v, uint32_t& lo, uint32_t& hi) {
+            const auto r2 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+            lo = r2[0]; hi = r2[1];
+        };
+        uint32_t t0, t1;
+        xch(p.gx, GX[0], GX[1]);
+        xch(__float_as_uint(p.fx), t0, t1); FX[0] = __uint_as_float(t0); FX[1] = __uint_as_float(t1);
+        xch(__float_as_uint(p.fy), t0, t1); FY[0] = __uint_as_float(t0); FY[1] = __uint_as_float(t1);
+        xch(__float_as_uint(p.fz), t0, t1); FZ[0] = __uint_as_float(t0); FZ[1] = __uint_as_float(t1);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) xch(rw[r], ROW[0][r], ROW[1][r]);
+    }
+    const bool load = valid && !(a.dbg & 128);
+    uint32_t off[8];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        const LvConst lc = lv_const(T, a.gm, u ? lb : la);
+        const uint32_t x = GX[u] + (uint32_t)h;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            uint32_t idx;
+            if (lc.dense) {
+                const uint32_t d = x + ROW[u][r];
+                idx = min(d, d - lc.hs);
+            } else {
+                idx = (x ^ ROW[u][r]) & (lc.hs - 1u);
+            }
+            const uint32_t ob = load ? lc.off : (RN_OOB >> 2);
+            off[4 * u + r] = (ob + idx) << 2;
+        }
+    }
+    uint32_t raw[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) raw[i] = __builtin_amdgcn_raw_buffer_load_b32(rs, off[i], 0, 0);
+    uint32_t res = 0u;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+        float a0 = 0.f, a1 = 0.f;
+        const float wx = h ? FX[u] : 1.0f - FX[u];
+        const float wy0 = 1.0f - FY[u], wz0 = 1.0f - FZ[u];
+        const float wxy0 = wx * wy0, wxy1 = wx * FY[u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const float w = ((r & 1) ? wxy1 : wxy0) * ((r >> 1) ? FZ[u] : wz0);
+            const uint32_t v = raw[4 * u + r];
+            a0 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v & 0xffffu)), a0);
+            a1 = fmaf(w, (float)__builtin_bit_cast(rn_half, (uint16_t)(v >> 16)), a1);
+        }
+        const auto s0 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a0), __float_as_uint(a0), false, false);
+        const auto s1 = __builtin_amdgcn_permlane32_swap(__float_as_uint(a1), __float_as_uint(a1), false, false);
+        const float v0 = __uint_as_float(s0[0]) + __uint_as_float(s0[1]);
+        const float v1 = __uint_as_float(s1[0]) + __uint_as_float(s1[1]);
+        const uint32_t pk = (uint32_t)__builtin_bit_cast(uint16_t, (rn_half)v0) |
+                            ((uint32_t)__builtin_bit_cast(uint16_t, (rn_half)v1) << 16);
+        if (u == h) res = pk;
+    }
+    return res;
+}
+
 // tcnn SphericalHarmonics degree 4 on (d/|d| + 1)/2 (networks.py:324-325)
 __device__ __forceinline__ half8 sh_lane(float dx, float dy, float dz, int h) {
     const float n = sqrtf(dx * dx + dy * dy + dz * dz);
@@ -359,7 +446,8 @@ __device__ __forceinline__ void mlp_forward(const rn_half* W, FwdState& st) {
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 enum { CACHE_NONE = 0, CACHE_WRITE = 1, CACHE_READ = 2,
-       CACHE_READ_NT = 3 };   // READ past L1: written by other waves of this kernel
+       CACHE_READ_NT = 3,     // READ past L1: written by other waves of this kernel
+       CACHE_PLANES = 4 };    // encoding from the level planes; the cache slot (if any) written
 
 // forward of one 32-sample tile for the lanes' samples `s` (valid lanes only
 // load); fc: this lane's encoding-cache slot (CACHE_WRITE writes it on every
@@ -375,6 +463,21 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
                                                int64_t s, bool valid, half8* fc, FwdState& st,
                                                float& ux, float& uy, float& uz) {
     float x = 0.f, y = 0.f, z = 0.f, dx = 1.f, dy = 0.f, dz = 0.f;
+    if (CACHE == CACHE_PLANES) {
+        // lane (c, h) holds levels lane_level(q, h), q = 0..7: e0 = q 0-3, e1 = q 4-7
+        const int h = rn_lane() >> 5;
+        typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+        u4v w0 = {0u, 0u, 0u, 0u}, w1 = {0u, 0u, 0u, 0u};
+        if (valid) {
+            const uint32_t* pl = a.planes + s;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                w0[q] = __builtin_nontemporal_load(pl + (size_t)lane_level(q, h) * a.plane_stride);
+                w1[q] = __builtin_nontemporal_load(pl + (size_t)lane_level(q + 4, h) * a.plane_stride);
+            }
+        }
+        st.e0 = __builtin_bit_cast(half8, w0); st.e1 = __builtin_bit_cast(half8, w1);
+    }
     if (valid) load_sample<MODE>(a, s, x, y, z, dx, dy, dz);
     tile_forward_pos<CACHE>(a, T, W, x, y, z, dx, dy, dz, valid, fc, st, ux, uy, uz);
 }
@@ -420,7 +523,10 @@ __device__ __forceinline__ void tile_forward_pos(const FieldArgs& a, const LvTab
     ux = unit_coord(x, a.xyz_min[0], a.extent[0]);
     uy = unit_coord(y, a.xyz_min[1], a.extent[1]);
     uz = unit_coord(z, a.xyz_min[2], a.extent[2]);
-    if (CACHE == CACHE_READ || CACHE == CACHE_READ_NT) {
+    if (CACHE == CACHE_PLANES) {
+        // st.e0 / st.e1 were loaded from the level planes (tile_forward_s)
+        if (valid && fc) { fc[0] = st.e0; fc[1] = st.e1; }
+    } else if (CACHE == CACHE_READ || CACHE == CACHE_READ_NT) {
         // lanes past the segment end (the backward walks whole 8-tile
         // iterations) were never written: zero encoding, as the gather path
         st.e0 = rn_zero8(); st.e1 = rn_zero8();

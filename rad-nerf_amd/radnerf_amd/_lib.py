@@ -64,6 +64,8 @@ SIGNATURES = {
     "rn_igrad_to_f32": [I64, P, P, P, P, P],
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,
                             P, P, I32, I32, P],
+    "rn_field_fwd_levels": [P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
+                            P, I64, P, I32, I32, P, P],
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, P, P, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],

@@ -76,6 +76,15 @@ class Workspace:
             self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
         return cap, self._chunks
 
+    def level_buffers(self):
+        """rn_field_fwd_levels' per-level encoding planes (16 x f16x2 per
+        sample slot, 64 B) and merged-order unit coordinates (16 B)."""
+        if getattr(self, "_levels", None) is None:
+            rows = self.feat.shape[0]
+            self._levels = (torch.empty(16, rows, device=self.device, dtype=torch.int32),
+                            torch.empty(rows, 4, device=self.device, dtype=torch.float32))
+        return self._levels
+
     def fx_buffers(self, n, device):
         """Fixed-point grid-gradient state (rn_grid_fx_fold): int32 sums (n,
         zero between steps), per-level scales (2, 16) (current / next, swapped
@@ -154,6 +163,12 @@ class FusedMLRenderer:
         # 16 waves: with the merged-order encode, C3 step 5.13 ms vs 5.16 at 8
         # (tools/step_variants.py, profiles/r01/step_variants_fwd_shape.json)
         self.merged_fwd_threads = 1024
+        # level-partitioned forward (rn_field_fwd_levels): each XCD encodes two
+        # levels of every sample, so its L2 holds two levels' tables; bit-exact
+        # with the merged forward (tools/enc_probe.py)
+        self.level_fwd = False
+        self.level_enc_blocks = 4096
+        self.level_mlp_blocks = 256
         self.merged_blocks = 256
         # chunk of merged samples per queue ticket: 1024 keeps a block's staged
         # rows L2-resident (C3 sweep: 768 3.94, 1024 3.88, 2048 3.92, 4096 4.05,
@@ -336,7 +351,15 @@ class FusedMLRenderer:
                   rays_d.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(), m.size,
                   m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
-        if fwd and self.merged_fwd:
+        if fwd and self.level_fwd:
+            planes, prep = w.level_buffers()
+            self._ev("field_fwd", L.field_fwd_levels, w.ts.data_ptr(), w.ray_of.data_ptr(),
+                     rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
+                     w.seg_count.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
+                     w.rgb.data_ptr(), w.feat.data_ptr(), w.mstart.data_ptr(), w.perm.data_ptr(),
+                     planes.data_ptr(), planes.shape[1], prep.data_ptr(), self.level_enc_blocks,
+                     self.level_mlp_blocks, None, st)
+        elif fwd and self.merged_fwd:
             self._ev("field_fwd", L.field_fwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w._chunk_desc.data_ptr(),

@@ -330,9 +330,11 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
     r = get_renderer(m, g, B)
     to = lambda a: torch.from_numpy(a).to(cuda)
     outs = []
-    # merged kernel with merged-order encoding, with per-tile encoding, per-model kernel
-    for merged, enc in ((True, True), (True, False), (False, False)):
-        r.merged_fwd, r.merged_encode = merged, enc
+    # merged kernel with merged-order encoding, with per-tile encoding, per-model
+    # kernel, level-partitioned forward (rn_field_fwd_levels)
+    for merged, enc, lv in ((True, True, False), (True, False, False), (False, False, False),
+                            (True, True, True)):
+        r.merged_fwd, r.merged_encode, r.level_fwd = merged, enc, lv
         ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=esf)
         w = r.ws
         off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
@@ -343,10 +345,42 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd, r.merged_encode = 1 < K <= 8, K > 1
+    r.merged_fwd, r.merged_encode, r.level_fwd = 1 < K <= 8, K > 1, False
     for o2 in outs[1:]:
         for a, b in zip(outs[0], o2):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("enc_blocks,mlp_blocks", [(8, 1), (24, 3), (8192, 512)])
+def test_level_forward_launch_shapes(cuda, enc_blocks, mlp_blocks):
+    """rn_field_fwd_levels with one block per level group (each block encodes
+    every tile of its two levels), ragged splits and more blocks than tiles:
+    bit-exact with the merged forward."""
+    B, K = 2048, 3
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=16.0)
+    r = get_renderer(m, g, B)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    outs = []
+    for lv in (False, True):
+        r.level_fwd = lv
+        r.level_enc_blocks, r.level_mlp_blocks = enc_blocks, mlp_blocks
+        ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=1 / 256)
+        w = r.ws
+        n = int(w.meta[0])
+        outs.append((w.sigma[:n].clone(), w.rgb[:n].clone(), w.feat.clone()))
+        w.feat.zero_()
+    r.level_fwd, r.level_enc_blocks, r.level_mlp_blocks = False, 4096, 256
+    w = r.ws
+    off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
+    idx = np.concatenate([np.arange(off[k, rr], off[k, rr] + cnt[k, rr])
+                          for k in range(K) for rr in range(B)]).astype(np.int64)
+    ii = torch.from_numpy(idx).to(cuda)
+    for a, b in zip(outs[0][:2], outs[1][:2]):
+        assert torch.equal(a[ii], b[ii])
+    feat = [f.view(-1, 64, 16) for f in (outs[0][2], outs[1][2])]
+    t, c = ii // 32, ii % 32
+    for h in (0, 32):
+        assert torch.equal(feat[0][t, c + h], feat[1][t, c + h])
 
 
 @pytest.mark.parametrize("mc,blocks,threads", [(64, 3, 256), (300, 37, 1024), (4096, 256, 512)])
