@@ -109,6 +109,9 @@ def parse():
     ap.add_argument("--grid-fx", type=int, default=None,
                     help="fixed-point grid-gradient accumulation: 1 on, 0 fp32 atomics "
                          "(default: the renderer's choice)")
+    ap.add_argument("--level-fwd", type=int, default=None,
+                    help="level-partitioned field forward (rn_field_fwd_levels): 1 on, 0 the "
+                         "merged forward (default: the renderer's choice)")
     ap.add_argument("--max-chunk", type=int, default=None,
                     help="merged backward: largest chunk of merged samples per queue grab "
                          "(default: the renderer's, by rays x sub-NeRFs)")
@@ -241,6 +244,8 @@ def main():
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     if args.grid_fx is not None:
         r.grid_fx = bool(args.grid_fx)
+    if args.level_fwd is not None:
+        r.level_fwd = bool(args.level_fwd)
     if args.max_chunk:
         r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk
@@ -557,6 +562,7 @@ def main():
                           "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,
                           "occupancy": args.occupancy,
                           "config": label,
+                          "field_fwd": "levels" if getattr(r, "level_fwd", False) else "merged",
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": (f"pinned{args.pinned_sim}-rank0-sim" if args.pinned_sim

@@ -26,6 +26,9 @@ void rn_set_debug_flags(int flags);
 /* ablation builds (debug flag 4096): per-phase wave cycles of the merged
  * backward, summed over waves, read and cleared (synchronous) */
 int rn_debug_cycles(unsigned long long* out);
+/* rn_field_fwd_levels' level groups for studies: byte g = levels (lo nibble,
+ * hi nibble) of group g, every level exactly once; 0 = default (g, 15 - g) */
+int rn_set_level_pairing(uint64_t pairing);
 
 /* ---- ray / AABB -----------------------------------------------------------
  * replaces vren.ray_aabb_intersect  (models/csrc/binding.cpp:4-16,
@@ -324,8 +327,9 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * f16x2 per level; blocks go to the XCDs round-robin, so each XCD's L2 holds
  * two levels' tables), then the per-model MLP tiles read the planes.
  * plane_stride > every sample index; enc_blocks a multiple of 8; mlp_blocks of
- * 1024 threads.  xq (optional, 64 int32): [8 g + x] = blocks of group g that
- * ran on XCD x (a probe of the mapping).  Replaces the same reference path as
+ * 1024 threads.  xq (optional, 96 int32): [8 g + x] = blocks of group g that
+ * ran on XCD x (a probe of the mapping), then u64 [32 + g] / [40 + g] the
+ * first start / last end of group g's blocks (s_memrealtime, 100 MHz).  Replaces the same reference path as
  * rn_field_fwd_merged (models/networks.py:300-328 via ml_rendering.py:174-179). */
 int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,

@@ -31,6 +31,7 @@
 #pragma clang fp contract(off)
 
 static int g_field_dbg = 0;
+static uint64_t g_level_pairing = 0;     // rn_field_fwd_levels' level groups (0 = default)
 // ablation builds only (flag 4096): per-phase wave cycles of the merged
 // backward, summed over waves (s_memtime): [0] MLP phase, [1] walk staging
 // (row loads + LDS fill, up to the barrier), [2] walks, [3] chunk tails
@@ -1414,17 +1415,20 @@ k_enc_prep(FieldArgs a, MergeArgs m, float4* __restrict__ prep) {
 
 __global__ void __launch_bounds__(256)
 k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
-                      int32_t* __restrict__ xq) {
+                      int32_t* __restrict__ xq, uint64_t pairing) {
     __shared__ LvTab sT;
     lv_stage(sT, a.gm);
     __syncthreads();
     const int g = blockIdx.x & 7;
-    if (xq && threadIdx.x == 0) {           // probe: group g's blocks per XCD
+    if (xq && threadIdx.x == 0) {           // probe: group g's blocks per XCD, its span
         uint32_t xcc;
         asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
         atomicAdd(xq + 8 * g + (int)(xcc & 7u), 1);
+        atomicMin(reinterpret_cast<unsigned long long*>(xq + 64) + g,
+                  (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
-    const int la = g, lb = RN_L - 1 - g;
+    // group g's levels: byte g of `pairing` (low nibble la, high lb)
+    const int la = (int)((pairing >> (8 * g)) & 15u), lb = (int)((pairing >> (8 * g + 4)) & 15u);
     const int P = m.mstart[m.n_rays];
     const int nt = (P + 31) >> 5;
     const int nb = (int)(gridDim.x >> 3), j = (int)(blockIdx.x >> 3);
@@ -1440,51 +1444,67 @@ k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
         const uint32_t v = encode_pair(a, sT, rs, h, la, lb, q.x, q.y, q.z, valid);
         if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
     }
+    if (xq) {
+        __syncthreads();
+        if (threadIdx.x == 0)
+            atomicMax(reinterpret_cast<unsigned long long*>(xq + 80) + g,
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
 }
 
-// MLP tiles of the K models (tile u: model k's 32 samples from seg_base[k] +
-// 32 t), waves strided over the flat tile list
-template <bool GW>
+// MLP tiles of the K models (tile u of the flat list: model k's 32 samples
+// from seg_base[k] + 32 t).  Block b takes a contiguous range of the list,
+// which spans one or two models at the bench sizes; their forward fragments
+// are staged in LDS, FM_LDS_K models at a time.
 __global__ void __launch_bounds__(1024)
 k_field_mlp_planes(FieldArgs a, int K) {
-    extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [K][24 frags]
+    extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [<= FM_LDS_K][24 frags]
     __shared__ LvTab sT;
-    if (!GW) {
-        for (int k = 0; k < K; ++k)
-            rn_block_copy16(sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
+    lv_stage(sT, a.gm);
+    int first[FM_KMAX + 1];
+    first[0] = 0;
+    for (int k = 0; k < K; ++k)
+        first[k + 1] = first[k] + ((__builtin_amdgcn_readfirstlane(a.seg_count[k]) + 31) >> 5);
+    const int T = first[K];
+    const int u0 = (int)((int64_t)T * blockIdx.x / gridDim.x);
+    const int u1 = (int)((int64_t)T * (blockIdx.x + 1) / gridDim.x);
+    if (u0 >= u1) return;                                   // block-uniform
+    int k_lo = 0, k_hi = 0;
+    for (int k = 0; k < K; ++k) {
+        if (first[k + 1] <= u0) k_lo = k + 1;
+        if (first[k] < u1) k_hi = k;
+    }
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), waves = blockDim.x >> 6;
+    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
+    for (int kb = k_lo; kb <= k_hi; kb += FM_LDS_K) {
+        const int ke = min(k_hi, kb + FM_LDS_K - 1);
+        __syncthreads();                                    // previous models' tiles done
+        for (int k = kb; k <= ke; ++k)
+            rn_block_copy16(sWm + (size_t)(k - kb) * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
                             a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
                             FIELD_FWD_FRAGS * RN_FRAG_BYTES);
-    }
-    lv_stage(sT, a.gm);
-    __syncthreads();
-    int nt[FM_KMAX];
-    int total = 0;
-    for (int k = 0; k < K; ++k) {
-        nt[k] = (__builtin_amdgcn_readfirstlane(a.seg_count[k]) + 31) >> 5;
-        total += nt[k];
-    }
-    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int W = (int)(gridDim.x * (blockDim.x >> 6));
-    const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
-    for (int u = (int)blockIdx.x * (int)(blockDim.x >> 6) + wid; u < total; u += W) {
-        int k = 0, t = u;
-        while (k < K - 1 && t >= nt[k]) { t -= nt[k]; ++k; }
-        const int n_k = a.seg_count[k];
-        const int i = t * 32 + c;
-        const bool valid = i < n_k;
-        const int64_t s = a.seg_base[k] + (valid ? i : 0);
-        FwdState st;
-        float ux, uy, uz;
-        const rn_half* Wk = GW ? a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS
-                               : sWm + (size_t)k * FIELD_FWD_FRAGS * RN_FRAG_HALFS;
-        rn_lds_order();
-        tile_forward_s<1, CACHE_PLANES>(a, sT, Wk, s, valid, a.feat ? cache_slot(a, s) : nullptr,
-                                        st, ux, uy, uz);
-        if (valid && h == 0) {
-            a.sigma[s] = expf(st.g0);
-            a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
-            a.rgb[3 * s + 1] = sigmoidf(st.out[1]);
-            a.rgb[3 * s + 2] = sigmoidf(st.out[2]);
+        __syncthreads();
+        const int ua = max(u0, first[kb]), ub = min(u1, first[ke + 1]);
+        for (int u = ua + wid; u < ub; u += waves) {
+            int k = kb;
+            while (k < ke && u >= first[k + 1]) ++k;
+            const int t = u - first[k];
+            const int n_k = a.seg_count[k];
+            const int i = t * 32 + c;
+            const bool valid = i < n_k;
+            const int64_t s = a.seg_base[k] + (valid ? i : 0);
+            FwdState st;
+            float ux, uy, uz;
+            rn_lds_order();
+            tile_forward_s<1, CACHE_PLANES>(a, sT, sWm + (size_t)(k - kb) * FIELD_FWD_FRAGS * RN_FRAG_HALFS,
+                                            s, valid, a.feat ? cache_slot(a, s) : nullptr, st,
+                                            ux, uy, uz);
+            if (valid && h == 0) {
+                a.sigma[s] = expf(st.g0);
+                a.rgb[3 * s + 0] = sigmoidf(st.out[0]);
+                a.rgb[3 * s + 1] = sigmoidf(st.out[1]);
+                a.rgb[3 * s + 2] = sigmoidf(st.out[2]);
+            }
         }
     }
 }
@@ -1985,6 +2005,16 @@ extern "C" {
 
 void rn_set_debug_flags(int flags) { g_field_dbg = flags; }
 
+int rn_set_level_pairing(uint64_t pairing) {
+    if (pairing != 0) {
+        uint32_t seen = 0;
+        for (int i = 0; i < 16; ++i) seen |= 1u << ((pairing >> (4 * i)) & 15u);
+        RN_CHECK_ARG(seen == 0xffffu, "pairing: every level exactly once");
+    }
+    g_level_pairing = pairing;
+    return 0;
+}
+
 /* ablation builds: read and clear the per-phase cycle counters (8 x u64) */
 int rn_debug_cycles(unsigned long long* out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rn_cyc), sizeof(unsigned long long) * 8, 0,
@@ -2244,8 +2274,9 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
    k_field_mlp_planes): the same outputs and encoding cache as
    rn_field_fwd_merged with the merged-order encoding.  planes: 16 x
    plane_stride u32 (plane_stride >= every sample index + 1); prep: 16 B per
-   merged sample; xq (optional probe): 64 int32, [8 g + x] += blocks of level
-   group g that ran on XCD x. */
+   merged sample; xq (optional probe): 96 int32, [8 g + x] += blocks of level
+   group g that ran on XCD x, then u64 [32 + g] first start and [40 + g] last
+   end of group g's blocks (s_memrealtime, 100 MHz). */
 int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         int64_t n_rays, int32_t n_models, const void* grid_f16,
@@ -2273,16 +2304,22 @@ int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* ray
     MergeArgs m{};
     m.mstart = mstart; m.perm = perm; m.n_rays = (int)n_rays; m.n_models = n_models;
     hipStream_t st = (hipStream_t)stream;
-    if (xq && hipMemsetAsync(xq, 0, 64 * sizeof(int32_t), st) != hipSuccess) {
+    if (xq && (hipMemsetAsync(xq, 0, 64 * sizeof(int32_t), st) != hipSuccess ||
+               hipMemsetAsync(xq + 64, 0xff, 16 * sizeof(int32_t), st) != hipSuccess ||
+               hipMemsetAsync(xq + 80, 0, 16 * sizeof(int32_t), st) != hipSuccess)) {
         rn_set_error("%s: probe reset failed", __func__);
         return 2;
     }
     k_enc_prep<<<1024, 256, 0, st>>>(a, m, (float4*)prep);
-    k_field_encode_levels<<<enc_blocks, 256, 0, st>>>(a, m, (const float4*)prep, xq);
-    const bool gw = n_models > FM_LDS_K;
-    if (gw) k_field_mlp_planes<true><<<mlp_blocks, 1024, 0, st>>>(a, n_models);
-    else k_field_mlp_planes<false><<<mlp_blocks, 1024,
-                                     (size_t)n_models * FIELD_FWD_FRAGS * RN_FRAG_BYTES, st>>>(a, n_models);
+    // level groups: (g, 15 - g) unless a study set another pairing (each level
+    // exactly once: checked on the host)
+    uint64_t pairing = g_level_pairing;
+    if (pairing == 0)
+        for (int g = 0; g < 8; ++g) pairing |= (uint64_t)(g | ((RN_L - 1 - g) << 4)) << (8 * g);
+    k_field_encode_levels<<<enc_blocks, 256, 0, st>>>(a, m, (const float4*)prep, xq, pairing);
+    k_field_mlp_planes<<<mlp_blocks, 1024,
+                         (size_t)min(n_models, FM_LDS_K) * FIELD_FWD_FRAGS * RN_FRAG_BYTES, st>>>(
+        a, n_models);
     RN_CHECK_LAUNCH();
     return 0;
 }

@@ -472,8 +472,8 @@ __device__ __forceinline__ void tile_forward_s(const FieldArgs& a, const LvTab& 
             const uint32_t* pl = a.planes + s;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                w0[q] = __builtin_nontemporal_load(pl + (size_t)lane_level(q, h) * a.plane_stride);
-                w1[q] = __builtin_nontemporal_load(pl + (size_t)lane_level(q + 4, h) * a.plane_stride);
+                w0[q] = pl[(size_t)lane_level(q, h) * a.plane_stride];
+                w1[q] = pl[(size_t)lane_level(q + 4, h) * a.plane_stride];
             }
         }
         st.e0 = __builtin_bit_cast(half8, w0); st.e1 = __builtin_bit_cast(half8, w1);

@@ -29,6 +29,7 @@ SIGNATURES = {
                         P, I32, P],
     "rn_field_density": [P, I64, P, P, P, P, P, P, P, P, P, P, P],
     "rn_debug_cycles": [P],
+    "rn_set_level_pairing": [ctypes.c_uint64],
     "rn_density_update_sampled": [P, P, I32, I32, I32, F32, F32, F32, U64, P, P, P, P, P, P, P,
                                   P, P, P, P, P, P, P],
     "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],

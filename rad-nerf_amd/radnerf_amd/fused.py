@@ -164,9 +164,12 @@ class FusedMLRenderer:
         # (tools/step_variants.py, profiles/r01/step_variants_fwd_shape.json)
         self.merged_fwd_threads = 1024
         # level-partitioned forward (rn_field_fwd_levels): each XCD encodes two
-        # levels of every sample, so its L2 holds two levels' tables; bit-exact
-        # with the merged forward (tools/enc_probe.py)
-        self.level_fwd = False
+        # levels of every sample, so its L2 holds two levels' tables instead of
+        # sixteen; bit-exact with the merged forward (tools/enc_probe.py).
+        # bench.py A/B (profiles/r03/lv_*_a1.json): C2 802 -> 853, C3 1098 ->
+        # 1139, C4 401 -> 450, C5 513 -> 549 M samples/s.  Needs the plan's
+        # merged order (rn_bwd_plan runs with the merged backward or forward).
+        self.level_fwd = self.merged_bwd or self.merged_fwd
         self.level_enc_blocks = 4096
         self.level_mlp_blocks = 256
         self.merged_blocks = 256
@@ -351,7 +354,7 @@ class FusedMLRenderer:
                   rays_d.data_ptr(), w.seg_base.data_ptr(), w.seg_count.data_ptr(), m.size,
                   m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
-        if fwd and self.level_fwd:
+        if fwd and self.level_fwd and (self.merged_bwd or self.merged_fwd):
             planes, prep = w.level_buffers()
             self._ev("field_fwd", L.field_fwd_levels, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),

@@ -345,7 +345,7 @@ def test_merged_forward_matches_per_model(cuda, B, K, scale):
         t, c = ii // 32, ii % 32
         cache = torch.stack([feat[t, c], feat[t, c + 32]], 1)
         outs.append((w.sigma[ii].clone(), w.rgb[ii].clone(), cache.clone()))
-    r.merged_fwd, r.merged_encode, r.level_fwd = 1 < K <= 8, K > 1, False
+    r.merged_fwd, r.merged_encode, r.level_fwd = 1 < K <= 8, K > 1, True
     for o2 in outs[1:]:
         for a, b in zip(outs[0], o2):
             assert torch.equal(a, b)
@@ -369,7 +369,7 @@ def test_level_forward_launch_shapes(cuda, enc_blocks, mlp_blocks):
         n = int(w.meta[0])
         outs.append((w.sigma[:n].clone(), w.rgb[:n].clone(), w.feat.clone()))
         w.feat.zero_()
-    r.level_fwd, r.level_enc_blocks, r.level_mlp_blocks = False, 4096, 256
+    r.level_fwd, r.level_enc_blocks, r.level_mlp_blocks = True, 4096, 256
     w = r.ws
     off, cnt = w.offsets.cpu().numpy(), w.counts.cpu().numpy()
     idx = np.concatenate([np.arange(off[k, rr], off[k, rr] + cnt[k, rr])
@@ -394,13 +394,13 @@ def test_merged_forward_chunking(cuda, mc, blocks, threads):
     to = lambda a: torch.from_numpy(a).to(cuda)
     outs = []
     for merged in (True, False):
-        r.merged_fwd, r.merged_encode = merged, merged
+        r.merged_fwd, r.merged_encode, r.level_fwd = merged, merged, False
         r.max_chunk, r.merged_fwd_blocks, r.merged_fwd_threads = mc, blocks, threads
         ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise))
         w = r.ws
         n = int(w.meta[0])
         outs.append((w.sigma[:n].clone(), w.rgb[:n].clone()))
-    r.merged_fwd, r.merged_encode, r.max_chunk = True, True, 1024
+    r.merged_fwd, r.merged_encode, r.max_chunk, r.level_fwd = True, True, 1024, True
     r.merged_fwd_blocks, r.merged_fwd_threads = 256, 1024
     # padding slots between segments are never written: compare the samples
     w = r.ws

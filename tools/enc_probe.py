@@ -44,7 +44,7 @@ def main():
     stride = w.feat.shape[0]
     planes = torch.zeros(16, stride, device=dev, dtype=torch.int32)
     prep = torch.zeros(stride, 4, device=dev, dtype=torch.float32)
-    xq = torch.zeros(64, device=dev, dtype=torch.int32)
+    xq = torch.zeros(96, device=dev, dtype=torch.int32)
     lo, lh, lr, ls = m.xyz_encoder.level_ptrs()
 
     def levels(eb, mb, probe=False):
@@ -82,7 +82,10 @@ def main():
            "rgb_mismatch": int((w.rgb.view(-1, 3)[s] != ref_rgb).sum().item()),
            "cache_mismatch": sum(int((F[s >> 5, (s & 31) + 32 * h] != ref_F[h]).sum().item())
                                  for h in (0, 1)),
-           "group_xcd_blocks": xq.view(8, 8).tolist()}
+           "group_xcd_blocks": xq[:64].view(8, 8).tolist()}
+    tt = xq[64:].view(torch.int64).cpu().numpy()
+    res["group_span_us"] = [round(float(tt[8 + i] - tt[i]) / 100.0, 1) for i in range(8)]
+    res["group_start_us"] = [round(float(tt[i] - tt[:8].min()) / 100.0, 1) for i in range(8)]
     t = {"fwd": []}
     for eb in blocks:
         for mb in mblocks:
