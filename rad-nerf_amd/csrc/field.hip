@@ -1436,12 +1436,13 @@ k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), waves = blockDim.x >> 6;
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = rn_rsrc(a.grid, a.grid_bytes);
+    const LvConst LA = lv_const_uniform(sT, a.gm, la), LB = lv_const_uniform(sT, a.gm, lb);
     uint32_t* const out = const_cast<uint32_t*>(a.planes) + (size_t)(h ? lb : la) * a.plane_stride;
     for (int t = t0 + wid; t < t1; t += waves) {
         const int p = t * 32 + c;
         const bool valid = p < P;
         const float4 q = prep[valid ? p : 0];
-        const uint32_t v = encode_pair(a, sT, rs, h, la, lb, q.x, q.y, q.z, valid);
+        const uint32_t v = encode_pair(a, rs, h, LA, LB, q.x, q.y, q.z, valid);
         if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
     }
     if (xq) {

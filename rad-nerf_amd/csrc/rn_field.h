@@ -277,31 +277,60 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
     for (int j = 0; j < 8; ++j) { e0[j] = (rn_half)f[j]; e1[j] = (rn_half)f[8 + j]; }
 }
 
+// A level's constants for a wave-uniform level index, in SGPRs
+__device__ __forceinline__ LvConst lv_const_uniform(const LvTab& T, const GridMeta& gm, int l) {
+    const LvConst c = lv_const(T, gm, l);
+    LvConst u;
+    u.off = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.off);
+    u.hs = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.hs);
+    u.res = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.res);
+    u.res2 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c.res2);
+    u.sc = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(c.sc)));
+    u.dense = c.dense;
+    return u;
+}
+
 // Two levels of the tile's 32 samples, the same arithmetic as encode_lane
-// (bit-identical features): wave half 0 computes level la's cell position
-// and row hashes, half 1 level lb's, v_permlane32_swap hands them across,
-// every lane gathers the 4 rows of its x-half for both levels, and the
-// x-halves are summed with a second swap.  Returns the features of level
-// (h ? lb : la) as packed f16x2 (feature 0 low).  la, lb wave-uniform.
-__device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, const LvTab& T,
-                                                __amdgpu_buffer_rsrc_t rs, int h, int la, int lb,
+// (bit-identical features): wave half 0 computes level A's cell position and
+// row hashes, half 1 level B's, v_permlane32_swap hands them across, every
+// lane gathers the 4 rows of its x-half for both levels, and the x-halves are
+// summed with a second swap.  Returns the features of level (h ? B : A) as
+// packed f16x2 (feature 0 low).  A, B: wave-uniform (lv_const_uniform), so
+// the dense / hashed choices are scalar branches or per-lane selects.
+__device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                                int h, const LvConst& A, const LvConst& Bc,
                                                 float ux, float uy, float uz, bool valid) {
     uint32_t GX[2], ROW[2][4];
     float FX[2], FY[2], FZ[2];
     {
-        const LvConst lm = lv_const(T, a.gm, h ? lb : la);
-        const LevelPos p = level_pos(lm.sc, ux, uy, uz);
+        const float sc = h ? Bc.sc : A.sc;
+        const uint32_t res = h ? Bc.res : A.res, res2 = h ? Bc.res2 : A.res2;
+        const LevelPos p = level_pos(sc, ux, uy, uz);
         uint32_t rw[4];
-        if (lm.dense) {
-            const uint32_t b = __umul24(p.gy, lm.res) + __umul24(p.gz, lm.res2);
+        auto dense_rows = [&](uint32_t* o) {
+            const uint32_t b = __umul24(p.gy, res) + __umul24(p.gz, res2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-                rw[r] = b + ((r & 1) ? lm.res : 0u) + ((r >> 1) ? lm.res2 : 0u);
-        } else {
+            for (int r = 0; r < 4; ++r) o[r] = b + ((r & 1) ? res : 0u) + ((r >> 1) ? res2 : 0u);
+        };
+        auto hashed_rows = [&](uint32_t* o) {
             const uint32_t y0 = p.gy * 2654435761u, z0 = p.gz * 805459861u;
             const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) rw[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
+            for (int r = 0; r < 4; ++r) o[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
+        };
+        const int dA = __builtin_amdgcn_readfirstlane((int)A.dense);
+        const int dB = __builtin_amdgcn_readfirstlane((int)Bc.dense);
+        if (dA && dB) {                          // scalar branches
+            dense_rows(rw);
+        } else if (!dA && !dB) {
+            hashed_rows(rw);
+        } else {                                 // one of each: both forms, selected per lane
+            uint32_t rd[4], rh[4];
+            dense_rows(rd);
+            hashed_rows(rh);
+            const bool dn = h ? dB : dA;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) rw[r] = dn ? rd[r] : rh[r];
         }
         auto xch = [&](uint32_t v, uint32_t& lo, uint32_t& hi) {
             const auto r2 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
@@ -319,19 +348,18 @@ __device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, const LvTab&
     uint32_t off[8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        const LvConst lc = lv_const(T, a.gm, u ? lb : la);
+        const LvConst& lc = u ? Bc : A;
         const uint32_t x = GX[u] + (uint32_t)h;
+        const uint32_t ob = load ? lc.off : (RN_OOB >> 2);
+        if (__builtin_amdgcn_readfirstlane((int)lc.dense)) {      // scalar branch
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            uint32_t idx;
-            if (lc.dense) {
+            for (int r = 0; r < 4; ++r) {
                 const uint32_t d = x + ROW[u][r];
-                idx = min(d, d - lc.hs);
-            } else {
-                idx = (x ^ ROW[u][r]) & (lc.hs - 1u);
+                off[4 * u + r] = (ob + min(d, d - lc.hs)) << 2;
             }
-            const uint32_t ob = load ? lc.off : (RN_OOB >> 2);
-            off[4 * u + r] = (ob + idx) << 2;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) off[4 * u + r] = (ob + ((x ^ ROW[u][r]) & (lc.hs - 1u))) << 2;
         }
     }
     uint32_t raw[8];

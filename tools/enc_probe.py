@@ -47,13 +47,14 @@ def main():
     xq = torch.zeros(96, device=dev, dtype=torch.int32)
     lo, lh, lr, ls = m.xyz_encoder.level_ptrs()
 
-    def levels(eb, mb, probe=False):
+    def levels(eb, mb, probe=False, feat=True):
         L.field_fwd_levels(w.ts.data_ptr(), w.ray_of.data_ptr(), o.data_ptr(), d.data_ptr(),
                            w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.B, m.size,
                            m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls,
                            m._h_min.ctypes.data, m._h_ext.ctypes.data,
                            m.packed_frags().data_ptr(), w.sigma.data_ptr(), w.rgb.data_ptr(),
-                           w.feat.data_ptr(), w.mstart.data_ptr(), w.perm.data_ptr(),
+                           w.feat.data_ptr() if feat else None, w.mstart.data_ptr(),
+                           w.perm.data_ptr(),
                            planes.data_ptr(), stride, prep.data_ptr(), eb, mb,
                            xq.data_ptr() if probe else None, st)
 
@@ -86,12 +87,13 @@ def main():
     tt = xq[64:].view(torch.int64).cpu().numpy()
     res["group_span_us"] = [round(float(tt[8 + i] - tt[i]) / 100.0, 1) for i in range(8)]
     res["group_start_us"] = [round(float(tt[i] - tt[:8].min()) / 100.0, 1) for i in range(8)]
-    t = {"fwd": []}
+    t = {"fwd": [], "lv_nofeat": []}
     for eb in blocks:
         for mb in mblocks:
             t[f"lv_{eb}_{mb}"] = []
     for _ in range(7):
         t["fwd"].append(timed(lambda: r._field(True, o, d, st)))
+        t["lv_nofeat"].append(timed(lambda: levels(blocks[0], mblocks[0], feat=False)))
         for eb in blocks:
             for mb in mblocks:
                 t[f"lv_{eb}_{mb}"].append(timed(lambda: levels(eb, mb)))

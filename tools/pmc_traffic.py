@@ -24,30 +24,32 @@ import sys
 from collections import defaultdict
 
 # the fused chain's kernels; the per-model kernels only where a run has no
-# merged launch (--split-bwd), never mixed (bench.py's drop-in leg runs them)
-KERNELS = {"field_bwd": ("k_field_bwd_merged", "k_field_bwd"),
-           "field_fwd": ("k_field_fwd_merged", "k_field_fwd")}
+# merged launch (--split-bwd), never mixed (bench.py's drop-in leg runs them).
+# An alternative is a tuple of kernels that together make one step's launch
+# (the level-partitioned forward: prep + encode + MLP tiles), summed.
+KERNELS = {"field_bwd": (("k_field_bwd_merged",), ("k_field_bwd",)),
+           "field_fwd": (("k_enc_prep", "k_field_encode_levels", "k_field_mlp_planes"),
+                         ("k_field_fwd_merged",), ("k_field_fwd",))}
 
 
 def per_dispatch(d):
     path = os.path.join(d, "run_counter_collection.csv")
-    vals = defaultdict(lambda: defaultdict(float))   # (kernel, pattern) -> dispatch -> value
+    vals = defaultdict(lambda: defaultdict(float))   # kernel pattern -> dispatch -> value
+    pats = {p for alts in KERNELS.values() for alt in alts for p in alt}
     with open(path) as f:
         for row in csv.DictReader(f):
             name = row.get("Kernel_Name", "")
             if "k_field_bwd_merged<" in name and name.split(">")[0].rstrip().endswith(", 3"):
                 continue        # the fixed-point redo launch (exits at once unless flagged)
-            for key, pats in KERNELS.items():
-                for pat in pats:
-                    if pat + "<" in name or pat + "(" in name:
-                        vals[(key, pat)][row["Dispatch_Id"]] += float(row["Counter_Value"])
-                        break
+            for pat in pats:
+                if pat + "<" in name or pat + "(" in name:
+                    vals[pat][row["Dispatch_Id"]] += float(row["Counter_Value"])
+                    break
     out = {}
-    for key, pats in KERNELS.items():
-        for pat in pats:
-            v = vals.get((key, pat))
-            if v:
-                out[key] = sum(v.values()) / len(v)
+    for key, alts in KERNELS.items():
+        for alt in alts:
+            if all(vals.get(p) for p in alt):
+                out[key] = sum(sum(vals[p].values()) / len(vals[p]) for p in alt)
                 break
     return out
 
