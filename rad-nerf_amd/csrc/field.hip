@@ -1438,10 +1438,18 @@ k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
     const __amdgpu_buffer_rsrc_t rs = rn_rsrc(a.grid, a.grid_bytes);
     const LvConst LA = lv_const_uniform(sT, a.gm, la), LB = lv_const_uniform(sT, a.gm, lb);
     uint32_t* const out = const_cast<uint32_t*>(a.planes) + (size_t)(h ? lb : la) * a.plane_stride;
+    // the next tile's prep row is loaded before this tile's gathers, so its
+    // latency overlaps theirs (one dependent round trip per tile, not two)
+    auto prep_row = [&](int t) {
+        const int p = t * 32 + c;
+        return prep[(t < t1 && p < P) ? p : 0];
+    };
+    float4 qn = prep_row(t0 + wid);
     for (int t = t0 + wid; t < t1; t += waves) {
         const int p = t * 32 + c;
         const bool valid = p < P;
-        const float4 q = prep[valid ? p : 0];
+        const float4 q = qn;
+        qn = prep_row(t + waves);
         const uint32_t v = encode_pair(a, rs, h, LA, LB, q.x, q.y, q.z, valid);
         if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
     }
