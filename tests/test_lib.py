@@ -58,6 +58,17 @@ def test_arg_validation_without_gpu():
         L.packbits(None, 8, 0.5, None, None)
     with pytest.raises(RuntimeError, match="n_params mismatch"):
         L.gate_bwd(None, None, 3, 10, 2, None, None, None, 5, None, None, 1, None)
+    # level-partitioned forward: level groups come in eights, at most 8 sub-NeRFs
+    lv = [None] * 6 + [8, 2] + [None] * 14 + [16, None]
+    with pytest.raises(RuntimeError, match="rn_field_fwd_levels.*multiple of 8"):
+        L.field_fwd_levels(*lv, 12, 1, None, None)
+    lv[7] = 9
+    with pytest.raises(RuntimeError, match="rn_field_fwd_levels.*n_models <= 8"):
+        L.field_fwd_levels(*lv, 16, 1, None, None)
+    # a level pairing must name every level exactly once
+    with pytest.raises(RuntimeError, match="every level exactly once"):
+        L.set_level_pairing(0x11)
+    assert L.set_level_pairing(0) == 0
 
 
 def test_vren_checks_like_reference():
