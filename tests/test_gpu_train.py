@@ -162,3 +162,24 @@ def test_batch_rays_match_reference_formula(cuda):
     o1, d1 = get_rays(dirs.to(cuda), poses[0].to(cuda))
     assert torch.allclose(d1.cpu().double(), dirs.double() @ poses[0, :, :3].double().T, atol=1e-6)
     assert torch.equal(o1.cpu(), poses[0, :, 3].expand(H * W, 3))
+
+
+def test_trainer_converges_fixed_point_like_fp32(cuda):
+    """End to end: trainer.Trainer (density updates with warm-up, fused render,
+    fused loss, merged backward, Adam) learns an analytic scene -- a coloured
+    sphere before the white background, fresh rays every step -- and the
+    fixed-point grid gradient trains like fp32 atomics (same init and rays).
+    tools/train_demo.py runs the long form (1000 steps: 35.9 vs 35.8 dB,
+    profiles/r03/train_demo_r03.json)."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "train_demo", os.path.join(os.path.dirname(__file__), "..", "tools", "train_demo.py"))
+    td = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(td)
+    fx = td.run(300, 4096, 2, True, cuda)
+    f32 = td.run(300, 4096, 2, False, cuda)
+    first, last = fx["curve"][0]["psnr"], fx["final_psnr"]
+    assert last > first + 10 and last > 28, fx["curve"]
+    assert abs(last - f32["final_psnr"]) < 0.5, (last, f32["final_psnr"])
+    assert fx["fx_redo_steps"] == 0
