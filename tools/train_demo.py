@@ -12,7 +12,7 @@ fixed-point grid gradient (the default) and with fp32 atomics, and the tool
 reports both loss curves, the PSNR of the rgb term and how many steps the
 fixed-point path redid in fp32.
 
-    python tools/train_demo.py [steps] [rays] [K]      -> one JSON line
+    python tools/train_demo.py [steps] [rays] [K] [scale]      -> one JSON line
 """
 import json
 import math
@@ -30,8 +30,8 @@ from radnerf_amd.trainer import Trainer  # noqa: E402
 R_SPHERE = 0.25
 
 
-def batch(gen, n, dev):
-    """rays + analytic targets (sphere hit -> 0.5 + 0.5 n, miss -> white)"""
+def batch(gen, n, dev, bg=1.0):
+    """rays + analytic targets (sphere hit -> 0.5 + 0.5 n, miss -> bg)"""
     u = torch.randn(n, 3, generator=gen, device=dev)
     o = 1.5 * u / u.norm(dim=1, keepdim=True)
     p = (torch.rand(n, 3, generator=gen, device=dev) * 2 - 1) * 0.4
@@ -44,13 +44,13 @@ def batch(gen, n, dev):
     hit = (disc > 0) & (t > 0)
     nrm = o + t[:, None] * d
     nrm = nrm / nrm.norm(dim=1, keepdim=True)
-    target = torch.where(hit[:, None], 0.5 + 0.5 * nrm, torch.ones_like(nrm))
+    target = torch.where(hit[:, None], 0.5 + 0.5 * nrm, torch.full_like(nrm, bg))
     return o.contiguous(), d.contiguous(), target.contiguous()
 
 
-def run(steps, B, K, grid_fx, dev):
+def run(steps, B, K, grid_fx, dev, scale=0.5):
     torch.manual_seed(0)
-    m = MNGP(0.5, size=K, seed=3).to(dev)
+    m = MNGP(scale, size=K, seed=3).to(dev)
     g = Ray_Gate(K, seed=4).to(dev)
     tr = Trainer(m, g, B, lr=1e-2, lambda_cv_importance=1e-2)
     tr.renderer.grid_fx = grid_fx
@@ -61,7 +61,8 @@ def run(steps, B, K, grid_fx, dev):
     torch.cuda.synchronize()
     t0 = time.time()
     for s in range(steps):
-        o, d, target = batch(gen, B, dev)
+        # train_ml.py's background: white at scale 0.5, black beyond (esf > 0)
+        o, d, target = batch(gen, B, dev, 1.0 if scale <= 0.5 else 0.0)
         terms = tr.step(o, d, d, target)
         if grid_fx and getattr(tr.renderer.ws, "_fx", None) is not None:
             redo_steps += int(tr.renderer.ws._fx[3].item())
@@ -84,14 +85,16 @@ def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     B = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
     K = int(sys.argv[3]) if len(sys.argv) > 3 else 2
+    scale = float(sys.argv[4]) if len(sys.argv) > 4 else 0.5
     dev = torch.device("cuda")
-    a = run(steps, B, K, True, dev)
-    b = run(steps, B, K, False, dev)
+    a = run(steps, B, K, True, dev, scale)
+    b = run(steps, B, K, False, dev, scale)
     pa, pb = a.pop("params"), b.pop("params")
     rel = float((pa - pb).norm() / pb.norm().clamp_min(1e-30))
-    print(json.dumps({"scene": f"sphere r={R_SPHERE} coloured 0.5+0.5n, white background, "
+    print(json.dumps({"scene": f"sphere r={R_SPHERE} coloured 0.5+0.5n, "
+                               f"{'white' if scale <= 0.5 else 'black'} background, "
                                "fresh random rays every step",
-                      "steps": steps, "rays": B, "models": K, "fixed_point": a, "fp32_atomics": b,
+                      "steps": steps, "rays": B, "models": K, "scale": scale, "fixed_point": a, "fp32_atomics": b,
                       "param_rel_l2_fx_vs_fp32": round(rel, 6)}))
 
 
