@@ -1389,7 +1389,7 @@ k_field_fwd_merged(FieldArgs a, MergeArgs m) {
 //   1. k_enc_prep: per merged position p the sample's unit coordinates and
 //      index (16 B), computed once (bit-identical to load_sample<1>);
 //   2. k_field_encode_levels: block b encodes levels g and 15 - g, g = b % 8,
-//      for every sample.  Workgroups are dispatched to the XCDs round-robin
+//      for every sample (one level after the other).  Workgroups are dispatched to the XCDs round-robin
 //      (a rotation that varies by dispatch: measured, group g ran on XCD
 //      g - 1 for all its blocks), so each XCD gathers from two levels' tables
 //      only; correctness does not depend on the mapping.  Output: one f16x2
@@ -1437,21 +1437,22 @@ k_field_encode_levels(FieldArgs a, MergeArgs m, const float4* __restrict__ prep,
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     const __amdgpu_buffer_rsrc_t rs = rn_rsrc(a.grid, a.grid_bytes);
     const LvConst LA = lv_const_uniform(sT, a.gm, la), LB = lv_const_uniform(sT, a.gm, lb);
-    uint32_t* const out = const_cast<uint32_t*>(a.planes) + (size_t)(h ? lb : la) * a.plane_stride;
-    // the next tile's prep row is loaded before this tile's gathers, so its
-    // latency overlaps theirs (one dependent round trip per tile, not two)
-    auto prep_row = [&](int t) {
-        const int p = t * 32 + c;
-        return prep[(t < t1 && p < P) ? p : 0];
-    };
-    float4 qn = prep_row(t0 + wid);
-    for (int t = t0 + wid; t < t1; t += waves) {
-        const int p = t * 32 + c;
-        const bool valid = p < P;
-        const float4 q = qn;
-        qn = prep_row(t + waves);
-        const uint32_t v = encode_pair(a, rs, h, LA, LB, q.x, q.y, q.z, valid);
-        if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
+    // level la over the block's tiles, then level lb: the XCD's blocks run in
+    // step, so its L2 holds one level's table at a time (two hashed levels at
+    // once, 4 MB, filled the whole L2).  A wave takes two tiles per pass.
+#pragma unroll 1
+    for (int ph = 0; ph < 2; ++ph) {
+        const LvConst& LC = ph ? LB : LA;
+        uint32_t* const out = const_cast<uint32_t*>(a.planes) + (size_t)(ph ? lb : la) * a.plane_stride;
+        for (int t = t0 + 2 * wid; t < t1; t += 2 * waves) {
+            const bool v0 = t * 32 + c < P;
+            const bool v1 = t + 1 < t1 && (t + 1) * 32 + c < P;
+            const bool valid = h ? v1 : v0;
+            const int p = (t + h) * 32 + c;
+            const float4 q = prep[valid ? p : 0];
+            const uint32_t v = encode_tiles(a, rs, h, LC, q.x, q.y, q.z, v0, v1);
+            if (valid) __builtin_nontemporal_store(v, out + __float_as_int(q.w));
+        }
     }
     if (xq) {
         __syncthreads();

@@ -290,47 +290,34 @@ __device__ __forceinline__ LvConst lv_const_uniform(const LvTab& T, const GridMe
     return u;
 }
 
-// Two levels of the tile's 32 samples, the same arithmetic as encode_lane
-// (bit-identical features): wave half 0 computes level A's cell position and
-// row hashes, half 1 level B's, v_permlane32_swap hands them across, every
-// lane gathers the 4 rows of its x-half for both levels, and the x-halves are
-// summed with a second swap.  Returns the features of level (h ? B : A) as
-// packed f16x2 (feature 0 low).  A, B: wave-uniform (lv_const_uniform), so
-// the dense / hashed choices are scalar branches or per-lane selects.
-__device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, __amdgpu_buffer_rsrc_t rs,
-                                                int h, const LvConst& A, const LvConst& Bc,
-                                                float ux, float uy, float uz, bool valid) {
+// One level of two tiles (32 samples each), the same arithmetic per (sample,
+// level) as encode_lane (bit-identical features): wave half h computes the
+// cell position and row hashes of sample c of tile h, v_permlane32_swap hands
+// them across, every lane gathers the 4 rows of its x-half for both tiles,
+// and the x-halves are summed with a second swap.  The level is wave-uniform
+// (lv_const_uniform): dense / hashed are scalar branches.  valid0 / valid1:
+// sample c of tile 0 / 1 exists (invalid samples gather nothing).  Returns
+// the features of the lane's own sample (tile h) as packed f16x2.
+// (Round 3 first paired two levels per tile instead: an XCD then gathered from
+// both its levels' tables at once, 4 MB for two hashed levels = its whole L2.)
+__device__ __forceinline__ uint32_t encode_tiles(const FieldArgs& a, __amdgpu_buffer_rsrc_t rs,
+                                                 int h, const LvConst& L, float ux, float uy,
+                                                 float uz, bool valid0, bool valid1) {
     uint32_t GX[2], ROW[2][4];
     float FX[2], FY[2], FZ[2];
+    const int dn = __builtin_amdgcn_readfirstlane((int)L.dense);
     {
-        const float sc = h ? Bc.sc : A.sc;
-        const uint32_t res = h ? Bc.res : A.res, res2 = h ? Bc.res2 : A.res2;
-        const LevelPos p = level_pos(sc, ux, uy, uz);
+        const LevelPos p = level_pos(L.sc, ux, uy, uz);
         uint32_t rw[4];
-        auto dense_rows = [&](uint32_t* o) {
-            const uint32_t b = __umul24(p.gy, res) + __umul24(p.gz, res2);
+        if (dn) {                                // scalar branch
+            const uint32_t b = __umul24(p.gy, L.res) + __umul24(p.gz, L.res2);
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = b + ((r & 1) ? res : 0u) + ((r >> 1) ? res2 : 0u);
-        };
-        auto hashed_rows = [&](uint32_t* o) {
+            for (int r = 0; r < 4; ++r) rw[r] = b + ((r & 1) ? L.res : 0u) + ((r >> 1) ? L.res2 : 0u);
+        } else {
             const uint32_t y0 = p.gy * 2654435761u, z0 = p.gz * 805459861u;
             const uint32_t y1 = y0 + 2654435761u, z1 = z0 + 805459861u;
 #pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
-        };
-        const int dA = __builtin_amdgcn_readfirstlane((int)A.dense);
-        const int dB = __builtin_amdgcn_readfirstlane((int)Bc.dense);
-        if (dA && dB) {                          // scalar branches
-            dense_rows(rw);
-        } else if (!dA && !dB) {
-            hashed_rows(rw);
-        } else {                                 // one of each: both forms, selected per lane
-            uint32_t rd[4], rh[4];
-            dense_rows(rd);
-            hashed_rows(rh);
-            const bool dn = h ? dB : dA;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) rw[r] = dn ? rd[r] : rh[r];
+            for (int r = 0; r < 4; ++r) rw[r] = ((r & 1) ? y1 : y0) ^ ((r >> 1) ? z1 : z0);
         }
         auto xch = [&](uint32_t v, uint32_t& lo, uint32_t& hi) {
             const auto r2 = __builtin_amdgcn_permlane32_swap(v, v, false, false);
@@ -344,22 +331,21 @@ __device__ __forceinline__ uint32_t encode_pair(const FieldArgs& a, __amdgpu_buf
 #pragma unroll
         for (int r = 0; r < 4; ++r) xch(rw[r], ROW[0][r], ROW[1][r]);
     }
-    const bool load = valid && !(a.dbg & 128);
+    const bool noload = a.dbg & 128;
     uint32_t off[8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-        const LvConst& lc = u ? Bc : A;
         const uint32_t x = GX[u] + (uint32_t)h;
-        const uint32_t ob = load ? lc.off : (RN_OOB >> 2);
-        if (__builtin_amdgcn_readfirstlane((int)lc.dense)) {      // scalar branch
+        const uint32_t ob = ((u ? valid1 : valid0) && !noload) ? L.off : (RN_OOB >> 2);
+        if (dn) {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const uint32_t d = x + ROW[u][r];
-                off[4 * u + r] = (ob + min(d, d - lc.hs)) << 2;
+                off[4 * u + r] = (ob + min(d, d - L.hs)) << 2;
             }
         } else {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) off[4 * u + r] = (ob + ((x ^ ROW[u][r]) & (lc.hs - 1u))) << 2;
+            for (int r = 0; r < 4; ++r) off[4 * u + r] = (ob + ((x ^ ROW[u][r]) & (L.hs - 1u))) << 2;
         }
     }
     uint32_t raw[8];

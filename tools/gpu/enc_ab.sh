@@ -4,7 +4,7 @@
 set -o pipefail
 tag=${1:-a}
 mkdir -p gpurun_out
-export ENC_BLOCKS=4096 MLP_BLOCKS=256
+export ENC_BLOCKS=${ENC_BLOCKS:-4096} MLP_BLOCKS=256
 Q="--dropin-step 0 --test-time-rays 0 --density-update 0 --cpu-rays 0 --train-step 0"
 timeout -k 10 150 python3 tools/enc_probe.py > gpurun_out/encab_c3_$tag.json 2> gpurun_out/encab_c3_$tag.err &&
 ABL_K=8 ABL_SCALE=16 ABL_RAYS=8192 timeout -k 10 150 python3 tools/enc_probe.py > gpurun_out/encab_c5_$tag.json 2> gpurun_out/encab_c5_$tag.err &&
