@@ -955,12 +955,14 @@ __device__ __forceinline__ void dw_park(float* p, const f32x16& A, const f32x16&
 #pragma unroll
     for (int j = 0; j < 16; ++j) { p[j * 64 + lane] = A[j]; p[(16 + j) * 64 + lane] = B[j]; }
 }
+// (read back past L1 with sc1 buffer loads: nt loads are slow on gfx950)
 __device__ __forceinline__ void dw_unpark(const float* p, f32x16& A, f32x16& B) {
-    const int lane = rn_lane();
+    const uint32_t lo = 4u * (uint32_t)rn_lane();
+    const __amdgpu_buffer_rsrc_t rs = rn_rsrc(p, 32 * 64 * 4);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-        A[j] = __builtin_nontemporal_load(p + j * 64 + lane);
-        B[j] = __builtin_nontemporal_load(p + (16 + j) * 64 + lane);
+        A[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lo + 256u * j, 0, 16));
+        B[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lo + 256u * (16 + j), 0, 16));
     }
 }
 
@@ -1041,6 +1043,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     uint64_t cyc[4] = {0, 0, 0, 0};
     float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
     float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
+    const __amdgpu_buffer_rsrc_t rows_rs = rn_rsrc(rows, (uint32_t)m.rows_cap * MB_ROW * 4u);
     int n_local = 0;
     int ticket = 0, n_chunks = 0;
     if (threadIdx.x == 0) { n_chunks = m.queue[1]; ticket = atomicAdd(m.queue, 1); }
@@ -1183,16 +1186,19 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 int k = 0;
                 for (int kq = 1; kq < K; ++kq) k = smp >= sCh[2 + 3 * MB_KMAX + kq] ? kq : k;
                 const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
-                // rows were written by other waves of this block: read past L1 (nt)
+                // rows were written by other waves of this block: read past L1
+                // with sc1 buffer loads (L2-served; the nt loads used before cost
+                // field_bwd 0.09 ms at C3, profiles/r03/rowab_*_r1.json)
                 typedef float nf4 __attribute__((ext_vector_type(4)));
                 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-                const float* rw = rows + (size_t)row_i * MB_ROW;
-                const nf4 u = __builtin_nontemporal_load(reinterpret_cast<const nf4*>(rw) + 4);
-                const h8* src = reinterpret_cast<const h8*>(rw) + 2 * half;
+                const uint32_t rb = (uint32_t)row_i * (MB_ROW * 4u);
+                const nf4 u = __builtin_bit_cast(nf4, __builtin_amdgcn_raw_buffer_load_b128(
+                    rows_rs, rb + 64u, 0, 16));
                 float* dst = sG + j * SG_STRIDE + 16 * half;
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
-                    const h8 v = __builtin_nontemporal_load(src + qq);
+                    const h8 v = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(
+                        rows_rs, rb + 16u * (2u * half + qq), 0, 16));
 #pragma unroll
                     for (int e2 = 0; e2 < 8; e2 += 2) {
                         const float a0 = (float)v[e2] * u.w, a1 = (float)v[e2 + 1] * u.w;
