@@ -178,10 +178,29 @@ def launch_check(args, rank, local, world):
     """--launch-check: the launcher's contract without GPU work."""
     check_world(args, world)
     seen = ranks_seen(rank, local, world, None, None)
+    # the headline N > 1 step's collective schedule on CPU tensors of the C3
+    # gradient shapes (grid 45.7 MB, MLP, gate): the early MLP + gate bucket,
+    # then the grid in args.buckets buckets, timed like the GPU run
+    comm = None
+    if world > 1:
+        from radnerf_amd import dist as rdist
+        from radnerf_amd import layout as LY
+        n_grid = 2 * int(LY.grid_levels(0.5)["n_entries"])
+        ar = rdist.GradAllReduce([torch.zeros(n_grid), torch.zeros(2, LY.FIELD_PARAMS),
+                                  torch.zeros(LY.gate_params(2))], "cpu")
+        for v in ar.views:
+            v.fill_(float(rank + 1))
+        hs = [ar.launch_range(*ar.param_range(1), 1),
+              ar.launch_range(*ar.param_range(0, 1), args.buckets)]
+        for h in hs:
+            ar.finish(h)
+        comm = ar.comm_stats(1)
+        comm["mean_ok"] = bool(torch.all(ar.flat == (world + 1) / 2))
+        comm["backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world,
                           "backend": dist.get_backend() if world > 1 else None,
-                          "ranks_seen": seen}), flush=True)
+                          "comm": comm, "ranks_seen": seen}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -252,22 +271,42 @@ def main():
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
 
+    # data parallel: the MLP + gate gradients (one small bucket) go out as soon
+    # as field_bwd has written them, beside the grid gradient's fold (or bin
+    # + sum); the grid gradient in args.buckets buckets after the backward.
+    # Both on a comm stream, bracketed by events there (comm fields below).
+    grid_rng, rest_rng = ar.param_range(0, 1), ar.param_range(1)
+    comm_on = [world > 1]
+    pending = []
+
+    def early_bucket():
+        if comm_on[0]:
+            main = torch.cuda.current_stream(dev)
+            main.wait_stream(r._side(dev))       # the gate backward ran on the side stream
+            pending.append(ar.launch_range(*rest_rng, 1))
+
+    r.after_field_bwd = early_bucket
+
     def step(i):
         ar.zero()
         _, _, _, gt, _ = r.forward(rays_o, rays_d, rays_d, noises[i % 4], bg, 1e-4, esf)
         samples_acc.add_(r.ws.meta[1])
         r.backward(rays_o, rays_d, rays_d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4,
                    grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
-        if world > 1:
-            # bucketed asynchronous all-reduce, each bucket averaged behind its
-            # own wait (pinned: partial gradients add up)
-            ar.reduce(average=not args.pinned, n_buckets=args.buckets)
+        if comm_on[0]:
+            if not pending:                      # (no merged backward: no early bucket)
+                pending.append(ar.launch_range(*rest_rng, 1))
+            pending.append(ar.launch_range(*grid_rng, args.buckets))
+            for h in pending:                    # pinned: partial gradients add up
+                ar.finish(h, average=not args.pinned)
+            pending.clear()
 
     log(f"rank {rank}/{world}: warm-up ({args.warmup} steps)")
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
     samples_acc.zero_()
+    ar.reset_timing()
     # timed region: HIP events only around the roofline kernel (an event pair
     # per launch costs ~5 us of queue time; all twelve would add ~2.5 %)
     r.trace = {"field_bwd"}
@@ -283,6 +322,30 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     bwd_live = r.kernel_times_ms()["field_bwd"]
+    comm = None
+    if world > 1:
+        # the collectives of the timed steps, then the same steps without them:
+        # exposed = what the all-reduce adds to the step (max over ranks)
+        comm = ar.comm_stats(args.steps)
+        comm_on[0] = False
+        dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            step(i)
+        torch.cuda.synchronize()
+        dist.barrier()
+        no_comm = torch.tensor(time.perf_counter() - t1, device=dev, dtype=torch.float64)
+        with_comm = torch.tensor(elapsed, device=dev, dtype=torch.float64)
+        dist.all_reduce(no_comm, op=dist.ReduceOp.MAX)
+        dist.all_reduce(with_comm, op=dist.ReduceOp.MAX)
+        comm_on[0] = True
+        comm.update({
+            "ms_per_step_without": round(float(no_comm) / args.steps * 1e3, 4),
+            "exposed_ms": round((float(with_comm) - float(no_comm)) / args.steps * 1e3, 4),
+            "backend": dist.get_backend(),
+            "schedule": "MLP+gate bucket after field_bwd (beside the grid fold), grid in "
+                        f"{args.buckets} buckets after the backward; comm stream events"})
     # per-kernel breakdown: the same steps again with every launch traced
     # (after the timed region; not part of `value`)
     r.trace = True
@@ -336,6 +399,7 @@ def main():
         params = [model.xyz_encoder.params, model.mlp_params, gate.params]
         for p_, v_ in zip(params, ar.views):
             p_.grad = v_
+        r.after_field_bwd = None        # reduce_and_step launches every bucket itself
         opt = FusedAdam(params, lr=1e-2, eps=1e-15)   # train_ml.py:143 (apex defaults)
         tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(7 + rank)).to(dev)
 
@@ -557,6 +621,7 @@ def main():
                "dtype": "f16/f32",
                "data": "synthetic",
                "backend": dist.get_backend() if world > 1 else None,
+               "comm": comm,
                "ranks_seen": seen,
                "config": {"workload": workload,
                           "rays_per_gpu": B, "model_zoo_size": K, "scale": scale,

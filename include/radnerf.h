@@ -19,6 +19,8 @@
 extern "C" {
 #endif
 
+#define RN_ABI_VERSION 2   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
 /* ablation switches for kernel studies (tools/ablate.py); 0 = production */
@@ -231,24 +233,29 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
                         int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
-                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_vmax,
-                        const int32_t* fx_redo, int32_t fx_mode, void* stream);
+                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_stats,
+                        const int32_t* fx_redo, int32_t fx_mode, void* gb_ctl,
+                        uint32_t* gb_page_meta, uint64_t* gb_pages, int32_t gb_pool_pages,
+                        void* stream);
 
 /* Fixed-point accumulation of the grid gradient (fx_mode 2, the fused
  * renderer's default; needs the encoding cache).  fx_acc: int32, one
  * per grid_grad element, zero on entry; fx_scale [16] f32 per level: 2^e_l, or
- * 0 for fp32 atomics into grid_grad (the first step); fx_vmax: the
- * 384-B per-level statistics block, zero before the first step: u32 vmax[16]
- * (the kernel atomic-maxes the bits of each level's largest |record|),
- * u32 emax[16] (rn_grid_fx_fold: the level's largest |int32 entry|),
- * i64 qsum[16] (the exact sum of each level's integer records),
- * i64 esum[16] (rn_grid_fx_fold: the exact sum of the level's int32 entries).
+ * 0 for fp32 atomics into grid_grad (the first step); fx_stats: the
+ * RN_FX_STATS_BYTES (640-B) per-level statistics block, zero before the first
+ * step: u32 vmax[16] (the kernel atomic-maxes the bits of each level's largest
+ * |record|), u32 emax[16] (rn_grid_fx_fold: the level's largest |int32 entry|),
+ * i64 qsum[16] (the exact sum of each level's integer records), i64 esum[16]
+ * (rn_grid_fx_fold: the exact sum of the level's int32 entries), u64 wq[16]
+ * and we[16] (the same sums with each element i weighted by
+ * (i * 2654435761) mod 2^32, mod 2^64).
  * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
  * memory side serves them ~27 % faster than f32 adds), so those levels'
  * gradients are order-independent and bitwise reproducible.
  * rn_grid_fx_fold then (1) sets *fx_redo when a level's largest record reached
  * 2^28 units or was not finite, or when the level's entry sum differs from its
- * record sum (an int32 entry wrapped: many same-sign records), writes the
+ * record sum, plain or weighted (an int32 entry wrapped: many same-sign
+ * records; two opposite wraps cancel only in the plain sum), writes the
  * next step's scales
  * (2^(23 - e), |record| < 2^e, capped so the largest entry stays < 2^28 units;
  * a dense level's first fixed-point step 2^(14 - e)) to fx_scale_next and clears
@@ -257,11 +264,50 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * fx_mode 3 and the same fx_scale (fp32 redo of the fixed-point levels' grid
  * scatter, no dW): it returns at once unless *fx_redo is set; and swaps
  * fx_scale_cur / fx_scale_next for the next step.
- * fx_mode 0: fp32 atomics (and the optional igrad_* integer mode).          */
+ * fx_mode 0: fp32 atomics (and the optional igrad_* integer mode).
+ * fx_mode 4: binned (rn_grid_bin below): the fixed-point records (int22, the
+ * largest < 2^18 units) are appended to the gb_* page pool (gb_ctl is reset
+ * by the call) instead of atomically added; rn_grid_binned_fold then bins
+ * and sums them into grid_grad (fx_acc unused).                            */
 int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
                     const uint32_t* level_res, int32_t* fx_acc, const float* fx_scale_cur,
                     float* fx_scale_next, uint32_t* fx_vmax, int32_t* fx_redo, float* grid_grad,
                     void* stream);
+
+/* Binned ("store and sum") grid-gradient scatter, passes 2 and 3
+ * (scatter.hip, formats in csrc/rn_bin.h).  Pass 1 is rn_field_bwd_merged
+ * with fx_mode 4: it appends each level's fixed-point records (u64: entry
+ * index 20 bits, two int22 features) to 64-KB pages of a pool instead of
+ * issuing memory-side atomics.  ctl: the 128-B GbCtl block (pages taken,
+ * pages per level), zero before pass 1; page_meta [pool_pages] u32 (level |
+ * count << 8); pages_in / pages_out [pool_pages][8192] u64; desc
+ * [pool_pages][128] u32; level_pages [16][pool_pages] u32.
+ * rn_grid_bin sorts each page by slice (8192 entries of its level) in LDS
+ * into pages_out and writes each slice's run (start | count << 16) to desc
+ * and the page to its level's list.  rn_grid_sum (one workgroup per slice,
+ * 64 KB of LDS) adds the slice's runs of every page of its level into int64
+ * accumulators (exact, order-free) and then grid_grad += acc * 2^-e_l
+ * (fx_scale) for every touched entry; it returns at once when *redo != 0.
+ * Replaces the hash-grid parameter gradient of the tcnn GridEncoding
+ * backward behind models/networks.py:300-328.                              */
+int rn_grid_bin_layout(int32_t* out);   /* host: page records, bins per page, slice
+                                          entries, ctl bytes, index bits, value bits */
+int rn_grid_bin(void* ctl, const uint32_t* page_meta, const uint64_t* pages_in,
+                uint64_t* pages_out, uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
+                int32_t blocks, void* stream);
+/* rn_grid_bin + the binned redo / scale check (a record at 2^21 units, a
+ * non-finite one, or a pool overflow sets *fx_redo; next scales 2^(18 - e))
+ * + rn_grid_sum, for a fx_mode 4 backward; the caller then launches the
+ * fx_mode 3 redo exactly as after rn_grid_fx_fold.                         */
+int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsize, void* ctl,
+                        const uint32_t* page_meta, const uint64_t* pages_in, uint64_t* pages_out,
+                        uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
+                        const float* fx_scale_cur, float* fx_scale_next, uint32_t* fx_stats,
+                        int32_t* fx_redo, float* grid_grad, void* stream);
+int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const void* ctl,
+                const uint32_t* desc, const uint32_t* level_pages, const uint64_t* pages_out,
+                int32_t pool_pages, const float* fx_scale, const int32_t* redo, float* grid_grad,
+                void* stream);
 
 /* Fused test-time render (ml_rendering.py:81-155 / rendering.py:113-189,
  * raymarching.cu:335-404, volumerendering.cu:206-286): one wave per ray marches
@@ -380,22 +426,25 @@ int rn_field_dinput(const float* xyzs, const float* dirs, int64_t n_samples, con
                     const void* frags, const void* dinput_frags, const float* dL_dsigma,
                     const float* dL_drgb, const void* feat_cache, float* dL_dxyz,
                     float* dL_ddir, int32_t blocks_per_model, void* stream);
-/* Sampled occupancy-grid update on the device (MNGP.update_density_grid
- * with warmup False, networks.py:345-409, train_ml.py:174-177), all n_models
- * sub-NeRFs and cascades in one call, no host synchronisation.  grid_ptrs /
- * bitfield_ptrs: device arrays of n_models pointers to the (cascades, 128^3)
- * f32 density grids (updated in place) and their bitfields.  Per (sub-NeRF,
- * cascade): the draws of 128^3/4 uniform cells and 128^3/4 cells among those
- * with density > threshold, as per-cell Poisson counts (rates 1/4 and
- * (128^3/4) / n_occupied, at most 31 per cell) from a counter-based hash of
- * `seed` (same seed -> same draws on every rank), listed and evaluated in cell
- * (Morton) order; each draw jittered in its cell; sigma from the grid + geo
- * MLP (frags: [n_models][46 * 512] f16); duplicates keep their max; then
+/* Occupancy-grid update on the device (MNGP.update_density_grid,
+ * networks.py:375-409, train_ml.py:174-177), all n_models sub-NeRFs and
+ * cascades in one call, no host synchronisation.  grid_ptrs / bitfield_ptrs:
+ * device arrays of n_models pointers to the (cascades, 128^3) f32 density
+ * grids (updated in place) and their bitfields.  all_cells != 0: every cell
+ * (the warm-up, networks.py:330-343); else per (sub-NeRF, cascade) the cells
+ * hit by 128^3/4 uniform draws and 128^3/4 draws among the cells with
+ * density > threshold (networks.py:345-372): cell j is drawn with
+ * probability 1 - e^-(1/4 + [occupied] (128^3/4) / n_occupied) (the
+ * multinomial counts' Poisson limit), decided by a counter-based hash of
+ * `seed` (same seed -> same cells on every rank).  Each drawn cell is
+ * evaluated ONCE, at a jittered point of its cell (the reference's index_put
+ * keeps one of a cell's draws, networks.py:394), in cell (Morton) order:
+ * sigma from the grid + geo MLP (frags: [n_models][46 * 512] f16); then
  * grid = grid < 0 ? grid : max(grid * decay, sampled), packbits at
  * min(mean of the positive cells, threshold) (thr_out [n_models]).
- * Scratch: tmp, occ (the draw list) (n_models * cascades * 128^3 f32 / i32),
- * blk (2 * (n_models * cascades * 128^3 / 1024 + 1) i32), part
- * (n_models * 1024 f32).  cascades <= 32.                                     */
+ * Scratch: tmp (the sampled sigma, 0 = not drawn), occ (the drawn-cell list)
+ * (n_models * cascades * 128^3 f32 / i32), blk (2 * (n_models * cascades *
+ * 128^3 / 1024 + 1) i32), part (n_models * 1024 f32).  cascades <= 32.      */
 int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, int32_t n_models,
                               int32_t cascades, int32_t grid_size, float scale,
                               float density_threshold, float decay, uint64_t seed,
@@ -403,7 +452,8 @@ int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, 
                               const uint32_t* level_hsize, const uint32_t* level_res,
                               const float* level_scale, const float* xyz_min, const float* extent,
                               const void* frags, float* tmp, int32_t* occ, int32_t* blk,
-                              float* part, float* thr_out, void* stream);
+                              float* part, float* thr_out, int32_t all_cells,
+                              void* stream);
 int rn_field_density(const float* xyzs, int64_t n_samples, const void* grid_f16,
                      const uint32_t* level_offset, const uint32_t* level_hsize,
                      const uint32_t* level_res, const float* level_scale, const float* xyz_min,

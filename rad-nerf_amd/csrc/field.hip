@@ -28,6 +28,7 @@
 // chain on MFMA, and form dW = dY . X^T block-cooperatively from sample-major
 // LDS images (MFMA again), held in registers across windows.
 #include "rn_field.h"
+#include "rn_bin.h"
 #pragma clang fp contract(off)
 
 static int g_field_dbg = 0;
@@ -299,6 +300,13 @@ struct Walk2 {
     // ... and the exact sum of the integer records issued for each (the
     // net-wrap check of rn_grid_fx_fold)
     int64_t sqA, sqB;
+    // ... and their position-weighted sum, sum of q * w(element) mod 2^64
+    // (fx_weight): two entries that wrap in opposite directions cancel in
+    // the plain sum but not in this one
+    uint64_t swA, swB;
+    // binned mode (GM 4): each level's open page in the pool and its fill,
+    // and the levels' first entries (wave-uniform)
+    uint32_t pgA, pgB, nA, nB, loffA, loffB;
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
@@ -324,6 +332,8 @@ struct IntGrad {
     int32_t* lo_ptr; int32_t* carry_ptr; const float* scale_ptr;
     uint32_t bytes;
     __amdgpu_buffer_rsrc_t fx;          // fixed-point mode (GM 2): FxGrad::acc
+    // binned mode (GM 4, rn_bin.h): the page pool the walk appends to
+    GbCtl* ctl; uint32_t* page_meta; uint64_t* pages; uint32_t pool_pages;
 };
 
 __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, uint32_t off,
@@ -361,13 +371,23 @@ struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats blo
     uint32_t emax[RN_L];   // largest |entry| this step, gradient units (float bits; rn_grid_fx_fold)
     int64_t qsum[RN_L];    // sum of the issued integer records
     int64_t esum[RN_L];    // sum of the int32 entries (rn_grid_fx_fold)
+    uint64_t wq[RN_L];     // sum of record * fx_weight(element), mod 2^64
+    uint64_t we[RN_L];     // sum of entry * fx_weight(element), mod 2^64 (rn_grid_fx_fold)
 };
+static_assert(sizeof(FxStats) == RN_FX_STATS_BYTES, "FxStats layout (include/radnerf.h)");
+
+// weight of grid-gradient element i (an int32 of the fixed-point table) in the
+// position-weighted checksums: a bijection of i mod 2^32 (odd multiplier), so
+// wraps of +-2^32 on two different elements a, b cancel only if w_a == w_b
+// (mod 2^32), i.e. never
+__host__ __device__ __forceinline__ uint32_t fx_weight(uint32_t i) { return i * 2654435761u; }
 
 struct FxGrad {
     int32_t* acc;              // int32 [entries][2]
     const float* scale;        // [RN_L] 2^e_l, 0 = fp32 atomics for the level
     uint32_t* vmax;            // FxStats::vmax
     int64_t* qsum;             // FxStats::qsum
+    uint64_t* wq;              // FxStats::wq
     const int32_t* redo;       // GM 3: the launch runs only when *redo != 0
     __amdgpu_buffer_rsrc_t rs; // over acc (built in the kernel)
 };
@@ -393,6 +413,23 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
     const bool fx_lvl = (scb << 1) != 0u;       // 2^e_l > 0: fixed point; +-0: fp32 atomics
     const float sc_s = __uint_as_float(scb);
     asm volatile("" ::: "memory");
+    if (GM == 4 && fx_lvl) {
+        // the level's open page cannot take cnt more records: close it (its
+        // level and fill, for the bin pass) and take the pool's next page
+        const uint32_t n = odd ? W.nB : W.nA;
+        if (n + cnt > GB_PAGE) {                         // wave-uniform
+            const uint32_t pg = odd ? W.pgB : W.pgA;
+            const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
+            const uint32_t lvl = odd ? RN_L - 1 - wid : wid;
+            uint32_t np = 0u;
+            if (lane == 0) {
+                if (pg < G.pool_pages) G.page_meta[pg] = lvl | (n << 8);
+                np = atomicAdd(&G.ctl->pool_next, 1u);
+            }
+            np = (uint32_t)__builtin_amdgcn_readlane((int)np, 0);
+            if (odd) { W.pgB = np; W.nB = 0u; } else { W.pgA = np; W.nA = 0u; }
+        }
+    }
     if (GM == 1) {
         // the issue two back has had a whole issue's time to return
         ig_check(W.oldA, W.loA, W.hiA, W.offA, G);
@@ -411,6 +448,25 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         } else if (dbg & 64) {      // ablation: non-returning i32 adds (timing only)
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
                 (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
+        } else if (GM == 4 && fx_lvl) {
+            // binned: the 32 records go to the level's open page as 32 u64
+            // (entry index, q0, q1), one 256-B store: lane 2r writes record
+            // r's low word, lane 2r + 1 its high word
+            const uint32_t ab = v & 0x7fffffffu;
+            if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
+            int q;
+            asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
+            q = min(max(q, -GB_V_MAX), GB_V_MAX);         // larger records: vmax flags a redo
+            const int qp = __builtin_amdgcn_mov_dpp(q, 0xb1, 0xf, 0xf, true);   // partner lane ^ 1
+            const uint32_t idx = (base[rec] >> 3) - (odd ? W.loffB : W.loffA);
+            const uint32_t q0 = (uint32_t)((lane & 1) ? qp : q), q1 = (uint32_t)((lane & 1) ? q : qp);
+            const uint32_t word = (lane & 1)
+                ? ((q0 >> 12) & 0x3ffu) | (q1 << 10)
+                : (idx & ((1u << GB_IDX_BITS) - 1u)) | (q0 << 20);
+            const uint32_t pg = odd ? W.pgB : W.pgA, n = odd ? W.nB : W.nA;
+            if (pg < G.pool_pages)
+                __builtin_nontemporal_store(
+                    word, reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane);
         } else if (GM == 2 && fx_lvl) {
             const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
@@ -420,7 +476,8 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             int q;
             asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
-            if (odd) W.sqB += (int64_t)q; else W.sqA += (int64_t)q;
+            const uint64_t wq = (uint64_t)((int64_t)q * (int64_t)fx_weight(off >> 2));
+            if (odd) { W.sqB += (int64_t)q; W.swB += wq; } else { W.sqA += (int64_t)q; W.swA += wq; }
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -431,7 +488,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             W.offB = off;
             W.oldB = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(lo, G.lo, (int)off, 0, 0);
         } else {
-            if (GM == 2) {                               // fp32 level: still tracked
+            if (GM == 2 || GM == 4) {                    // fp32 level: still tracked
                 const uint32_t ab = v & 0x7fffffffu;
                 if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             }
@@ -440,6 +497,9 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         }
     }
     asm volatile("" ::: "memory");
+    if (GM == 4 && fx_lvl) {
+        if (odd) W.nB += cnt; else W.nA += cnt;
+    }
     const bool me = (lane >> 2) == s;                     // selects, not a branch
     W.head = me ? w2_wrap(W.head + cnt) : W.head;
     W.pend = me ? W.pend - cnt : W.pend;
@@ -1008,6 +1068,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
     int64_t sqA = 0, sqB = 0;
+    uint64_t swA = 0, swB = 0;
+    // binned mode: this wave's open pages (none yet: the first issue takes one)
+    uint32_t pgA = 0xffffffffu, pgB = 0xffffffffu, nA = GB_PAGE, nB = GB_PAGE;
     if (GM >= 2) {
         fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
         fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
@@ -1169,6 +1232,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         Walk2 W;
         walk2_begin(W, ring2);
         W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB; W.sqA = sqA; W.sqB = sqB;
+        W.swA = swA; W.swB = swB;
+        W.pgA = pgA; W.pgB = pgB; W.nA = nA; W.nB = nB;
+        W.loffA = sT.off[wid]; W.loffB = sT.off[RN_L - 1 - wid];
         sw_ok = false;                           // the staging overwrites sW
         for (int w0 = 0; w0 < E; w0 += MB_WIN) {
           int nz = 0;
@@ -1225,20 +1291,29 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         walk2_end<GM>(a, sT, grad_rs, G, W, dbg);
         if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[3] += t - tp0; tp0 = t; }
         vmA = W.vmA; vmB = W.vmB; sqA = W.sqA; sqB = W.sqB;
+        swA = W.swA; swB = W.swB;
+        pgA = W.pgA; pgB = W.pgB; nA = W.nA; nB = W.nB;
         __syncthreads();                         // rings (image region) drained
     }
     if (ABL && (dbg & 4096) && rn_lane() == 0) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
     }
-    if (GM == 2) {                               // this step's largest |record| per level
+    if (GM == 4 && rn_lane() == 0) {             // close this wave's open pages
+        if (pgA < G.pool_pages) G.page_meta[pgA] = (uint32_t)wid | (nA << 8);
+        if (pgB < G.pool_pages) G.page_meta[pgB] = (uint32_t)(RN_L - 1 - wid) | (nB << 8);
+    }
+    if (GM == 2 || GM == 4) {                    // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
         vmB = rn_wave_max_u32(vmB);
         int64_t dA = sqA, dB = sqB;
+        uint64_t eA = swA, eB = swB;
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             dA += __shfl_xor(dA, off);
             dB += __shfl_xor(dB, off);
+            eA += __shfl_xor(eA, off);
+            eB += __shfl_xor(eB, off);
         }
         if (rn_lane() == 0) {
             if (vmA) atomicMax(F.vmax + wid, vmA);
@@ -1247,6 +1322,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                                    (unsigned long long)dA);
             if (dB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + RN_L - 1 - wid),
                                    (unsigned long long)dB);
+            if (eA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + wid), eA);
+            if (eB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + RN_L - 1 - wid), eB);
         }
     }
     // ---- flush every model's dW (the current one from registers)
@@ -1582,6 +1659,7 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
     typedef int vi4 __attribute__((ext_vector_type(4)));
     const int64_t e0 = 2 * (int64_t)gm.offset[l], n4 = (2 * (int64_t)gm.hsize[l]) >> 2;
     int64_t s = 0;
+    uint64_t ws = 0;                 // sum of entry * fx_weight(element), mod 2^64
     uint32_t mx = 0u;           // fixed point: |int|; fp32 level: |float| bits
     auto uabs = [](int x) { return x < 0 ? 0u - (uint32_t)x : (uint32_t)x; };
     if (sc != 0.f) {
@@ -1590,6 +1668,11 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
              i += (int64_t)gridDim.x * blockDim.x) {
             const vi4 v = __builtin_nontemporal_load(a4 + i);
             s += (int64_t)v.x + v.y + v.z + v.w;
+            const uint32_t el = (uint32_t)(e0 + 4 * i);
+            ws += (uint64_t)((int64_t)v.x * (int64_t)fx_weight(el)) +
+                  (uint64_t)((int64_t)v.y * (int64_t)fx_weight(el + 1)) +
+                  (uint64_t)((int64_t)v.z * (int64_t)fx_weight(el + 2)) +
+                  (uint64_t)((int64_t)v.w * (int64_t)fx_weight(el + 3));
             mx = max(max(mx, max(uabs(v.x), uabs(v.y))), max(uabs(v.z), uabs(v.w)));
         }
     } else {
@@ -1604,17 +1687,21 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
         s += __shfl_xor(s, off);
+        ws += __shfl_xor(ws, off);
         mx = max(mx, (uint32_t)__shfl_xor((int)mx, off));
     }
     // one atomic per block (per-wave atomics on the level words serialised:
     // 107 us for 16k of them)
     __shared__ int64_t sW[4];
+    __shared__ uint64_t sWw[4];
     __shared__ uint32_t sM[4];
     const int w = threadIdx.x / RN_WAVE;
-    if (rn_lane() == 0) { sW[w] = s; sM[w] = mx; }
+    if (rn_lane() == 0) { sW[w] = s; sWw[w] = ws; sM[w] = mx; }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int64_t t = (sW[0] + sW[1]) + (sW[2] + sW[3]);
+        const uint64_t tw = (sWw[0] + sWw[1]) + (sWw[2] + sWw[3]);
+        if (tw != 0) atomicAdd(reinterpret_cast<unsigned long long*>(st->we + l), tw);
         uint32_t m = max(max(sM[0], sM[1]), max(sM[2], sM[3]));
         if (sc != 0.f) m = __float_as_uint((float)m / sc);     // units -> gradient units
         if (t != 0) atomicAdd(reinterpret_cast<unsigned long long*>(st->esum + l), (unsigned long long)t);
@@ -1643,19 +1730,31 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 #define FX_ENTRY_BITS 28
 #define FX_DENSE_FIRST_BITS 14
 #define FX_GROWTH_UNITS 268435456.f       // 2^28
+// Binned mode (ctl != NULL, rn_grid_binned_fold): records are int22, summed
+// exactly in int64, so there is no entry cap and no wrap check; the largest
+// record maps to < 2^GB_TARGET_BITS units (8x headroom below the int22 range,
+// like round 2's 2^19 / 2^22), a record at 2^21 units or a pool overflow (the
+// walk ran out of pages) sets the redo flag.
 __global__ void __launch_bounds__(64)
 k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
            float* __restrict__ scale_next, FxStats* __restrict__ stats,
-           int32_t* __restrict__ redo) {
+           int32_t* __restrict__ redo, const GbCtl* __restrict__ ctl, uint32_t pool_pages) {
     const int l = threadIdx.x;
     uint32_t* vmax = stats->vmax;
-    bool bad = false;
+    const bool binned = ctl != nullptr;
+    bool bad = binned && l == 0 && ctl->pool_next > pool_pages;
+    const float growth = binned ? (float)(GB_V_MAX + 1) : FX_GROWTH_UNITS;
     if (l < RN_L) {
         // net wrap of an int32 entry: the entries' exact sum differs from the
         // records' exact sum (by a multiple of 2^32)
-        if (scale_cur[l] != 0.f && stats->esum[l] != stats->qsum[l]) bad = true;
+        // (and the position-weighted sums: opposite wraps cancel only in the plain one)
+        if (!binned && scale_cur[l] != 0.f &&
+            (stats->esum[l] != stats->qsum[l] || stats->we[l] != stats->wq[l]))
+            bad = true;
         stats->esum[l] = 0;
         stats->qsum[l] = 0;
+        stats->we[l] = 0;
+        stats->wq[l] = 0;
         const uint32_t vb = vmax[l];
         const float sc = scale_cur[l];
         const uint32_t em = stats->emax[l];
@@ -1665,11 +1764,13 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
             bad = bad || sc != 0.f;
         } else if (vb != 0u) {
             const float v = __uint_as_float(vb);
-            bad = bad || (sc != 0.f && v * sc >= FX_GROWTH_UNITS);
+            bad = bad || (sc != 0.f && v * sc >= growth);
             int e;
             frexpf(v, &e);                               // v < 2^e
-            int bits = FX_TARGET_BITS - e;
-            if (em != 0u) {                              // the largest entry stays < 2^28 units
+            int bits = (binned ? GB_TARGET_BITS : FX_TARGET_BITS) - e;
+            if (binned) {
+                // int64 sums: no entry cap
+            } else if (em != 0u) {                       // the largest entry stays < 2^28 units
                 int ee;
                 frexpf(__uint_as_float(em), &ee);
                 bits = min(bits, FX_ENTRY_BITS - ee);
@@ -2020,6 +2121,9 @@ inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 extern "C" {
 
 void rn_set_debug_flags(int flags) { g_field_dbg = flags; }
+}  // extern "C"
+int rn_debug_flags_internal() { return g_field_dbg; }
+extern "C" {
 
 int rn_set_level_pairing(uint64_t pairing) {
     if (pairing != 0) {
@@ -2170,12 +2274,22 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         float* grid_grad, float* dw, const void* feat_cache, float* scratch,
                         int64_t scratch_rows, float* park, int32_t max_chunk, int32_t blocks,
                         int32_t* igrad_lo, int32_t* igrad_carry, const float* igrad_scale,
-                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_vmax,
-                        const int32_t* fx_redo, int32_t fx_mode, void* stream) {
+                        int32_t* fx_acc, const float* fx_scale, uint32_t* fx_stats,
+                        const int32_t* fx_redo, int32_t fx_mode, void* gb_ctl,
+                        uint32_t* gb_page_meta, uint64_t* gb_pages, int32_t gb_pool_pages,
+                        void* stream) {
     RN_CHECK_ARG(!igrad_lo || (igrad_carry && igrad_scale), "integer mode needs carry and scale");
-    RN_CHECK_ARG(fx_mode == 0 || fx_mode == 2 || fx_mode == 3, "fx_mode: 0, 2 or 3");
-    RN_CHECK_ARG(fx_mode != 2 || (fx_acc && fx_scale && fx_vmax && feat_cache),
-                 "fixed-point mode needs acc, scale, vmax and the encoding cache");
+    RN_CHECK_ARG(fx_mode == 0 || fx_mode == 2 || fx_mode == 3 || fx_mode == 4,
+                 "fx_mode: 0, 2, 3 or 4");
+    RN_CHECK_ARG(fx_mode != 2 || (fx_acc && fx_scale && fx_stats && feat_cache),
+                 "fixed-point mode needs acc, scale, stats and the encoding cache");
+    RN_CHECK_ARG(fx_mode != 4 || (fx_scale && fx_stats && feat_cache && gb_ctl && gb_page_meta &&
+                                  gb_pages && gb_pool_pages >= 1),
+                 "binned mode needs scale, stats, the encoding cache and the page pool");
+    for (int l = 0; fx_mode == 4 && l < RN_L; ++l)
+        RN_CHECK_ARG(level_hsize[l] <= (1u << GB_IDX_BITS) &&
+                     level_hsize[l] <= ((uint32_t)GB_MAX_BINS << GB_SLICE_BITS),
+                     "binned mode: a level has more than 2^20 entries");
     RN_CHECK_ARG(fx_mode != 3 || (fx_redo && fx_scale && feat_cache),
                  "fixed-point redo needs the redo flag, the step's scales and the encoding cache");
     RN_CHECK_ARG(!(igrad_lo && fx_mode), "integer and fixed-point modes are exclusive");
@@ -2211,14 +2325,27 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         G.bytes = 2 * a.grid_bytes;            // int32 arrays, same size as the f32 grad
         G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
     }
+    if (fx_mode == 4) {
+        if (hipMemsetAsync(gb_ctl, 0, sizeof(GbCtl), st) != hipSuccess) {
+            rn_set_error("%s: page pool reset failed", __func__);
+            return 2;
+        }
+        G.ctl = (GbCtl*)gb_ctl; G.page_meta = gb_page_meta; G.pages = gb_pages;
+        G.pool_pages = (uint32_t)gb_pool_pages;
+    }
     FxGrad F{};
     F.acc = fx_acc; F.scale = fx_scale; F.redo = fx_redo;
-    if (fx_vmax) {
-        F.vmax = reinterpret_cast<FxStats*>(fx_vmax)->vmax;
-        F.qsum = reinterpret_cast<FxStats*>(fx_vmax)->qsum;
+    if (fx_stats) {
+        F.vmax = reinterpret_cast<FxStats*>(fx_stats)->vmax;
+        F.qsum = reinterpret_cast<FxStats*>(fx_stats)->qsum;
+        F.wq = reinterpret_cast<FxStats*>(fx_stats)->wq;
     }
     const dim3 blk(BWD_WAVES * 64);
-    if (fx_mode == 2 && a.dbg) {
+    if (fx_mode == 4 && a.dbg) {
+        k_field_bwd_merged<CACHE_READ, true, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (fx_mode == 4) {
+        k_field_bwd_merged<CACHE_READ, false, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (fx_mode == 2 && a.dbg) {
         k_field_bwd_merged<CACHE_READ, true, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (fx_mode == 2) {
         k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
@@ -2377,7 +2504,7 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
     hipStream_t st = (hipStream_t)stream;
     FxStats* stats = reinterpret_cast<FxStats*>(fx_vmax);
     k_fx_esum<<<dim3(128, RN_L), 256, 0, st>>>(gm, fx_scale_cur, fx_acc, grid_grad, stats);
-    k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo);
+    k_fx_check<<<1, 64, 0, st>>>(hashed, fx_scale_cur, fx_scale_next, stats, fx_redo, nullptr, 0u);
     RN_CHECK_LAUNCH();
     {   // every level (dense ones go fixed point from their second step)
         const int64_t e0 = 2 * (int64_t)level_offset[0];
@@ -2391,6 +2518,19 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
     }
     return 0;
 }
+
+}  // extern "C"
+
+int rn_fx_check_binned(const float* fx_scale_cur, float* fx_scale_next, uint32_t* fx_stats,
+                       int32_t* fx_redo, const void* ctl, uint32_t pool_pages, void* stream) {
+    k_fx_check<<<1, 64, 0, (hipStream_t)stream>>>(0u, fx_scale_cur, fx_scale_next,
+                                                  reinterpret_cast<FxStats*>(fx_stats), fx_redo,
+                                                  (const GbCtl*)ctl, pool_pages);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+extern "C" {
 
 int rn_igrad_to_f32(int64_t n, int32_t* igrad_lo, int32_t* igrad_carry, const float* scale,
                     float* grid_grad, void* stream) {

@@ -313,19 +313,20 @@ k_field_density(FieldArgs a, float* __restrict__ feat_out) {
 // warmup False, all K sub-NeRFs and C cascades per launch, no host sync).
 // The reference draws, per (sub-NeRF k, cascade c), M = G^3/4 uniform cells
 // and M cells uniformly among those with density > threshold (with
-// replacement), jitters each in its cell and evaluates sigma there.  What the
-// update keeps of a cell is the max over its draws, so only the NUMBER of
-// draws per cell and their jitters matter: here every cell j gets
-// n_j = Poisson(M / G^3) + [occupied] Poisson(M / n_occupied) draws (the
-// limit of the multinomial counts; hit rates 1 - e^-1/4 and 1 - e^-(1/4 +
-// M/n_o) as the reference's), from a counter-based hash of (seed, k, c, j)
-// instead of torch's generator (identical on every rank for the same seed).
-// The draws are listed in cell (Morton) order and evaluated in that order, so
-// consecutive samples share grid lines as the warm-up's ordered sweep does
-// (random placement cost ~2x per sample: DESIGN.md §4).
+// replacement), jitters each in its cell, evaluates sigma there and writes it
+// with an index_put (density_grid_tmp[c, indices] = sigma, networks.py:394):
+// a cell drawn several times keeps ONE of its draws (whichever write lands
+// last), and all draws of a cell are i.i.d. jittered points.  So what matters
+// per cell is only WHETHER it is drawn, and at which jittered point: here
+// cell j of segment (k, c) is drawn with probability 1 - e^-(M / G^3 +
+// [occupied] M / n_occupied) (the multinomial counts' Poisson limit: the
+// reference's hit rates), decided by a counter-based hash of (seed, k, c, j)
+// instead of torch's generator (identical on every rank for the same seed),
+// and evaluated once, at the jitter of its first draw.  The drawn cells are
+// listed in cell (Morton) order and evaluated in that order, so consecutive
+// samples share grid lines as the warm-up's ordered sweep does.
 // ---------------------------------------------------------------------------
 #define DU_BLK 1024        // cells per counting block (G^3 is a multiple)
-#define DU_DUP_MAX 31      // draws of one cell kept (5 bits of the list entry)
 
 __device__ __forceinline__ uint64_t du_mix(uint64_t z) {      // splitmix64 finaliser
     z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -338,34 +339,23 @@ __device__ __forceinline__ uint32_t du_hash(uint64_t seed, uint32_t seg, uint32_
 }
 __device__ __forceinline__ float du_unit(uint32_t h) { return (float)(h >> 8) * (1.0f / 16777216.0f); }
 
-// a Poisson(lam) count from the uniform words h (inverse CDF below rate 16;
-// above it the normal approximation, Box-Muller with h2), capped
-__device__ __forceinline__ uint32_t du_poisson(float lam, uint32_t h, uint32_t h2) {
-    if (!(lam > 0.f)) return 0u;
-    if (lam < 16.f) {
-        const float u = du_unit(h);
-        float p = expf(-lam), cdf = p;
-        uint32_t k = 0;
-        while (u > cdf && k < DU_DUP_MAX) { ++k; p *= lam / (float)k; cdf += p; }
-        return k;
-    }
-    const float u1 = fmaxf(du_unit(h), 1.0f / 16777216.0f), u2 = du_unit(h2);
-    const float z = sqrtf(-2.0f * logf(u1)) * cosf(6.28318530718f * u2);
-    const float v = floorf(lam + sqrtf(lam) * z + 0.5f);
-    return v <= 0.f ? 0u : (uint32_t)fminf(v, (float)DU_DUP_MAX);
+// a draw with probability 1 - e^-lam from the uniform word h
+__device__ __forceinline__ bool du_hit(float lam, uint32_t h) {
+    return lam > 0.f && du_unit(h) >= expf(-lam);
 }
 
 struct DensityUpd {
     const float* const* grids;      // [K] -> (C, G3) density grids
     uint8_t* const* bitfields;      // [K] -> C G3 / 8 bytes
     float* tmp;                     // (K, C, G3) sampled sigma, zero on entry
-    uint32_t* list;                 // (K C G3) draws, cell-ordered: cell | d << 21 | c << 26
+    uint32_t* list;                 // (K C G3) drawn cells, cell-ordered: cell | c << 26
     int32_t* blk;                   // (K C G3 / DU_BLK + 1) occupied counts -> offsets
     int32_t* dblk;                  // (K C G3 / DU_BLK + 1) draw counts -> offsets
     float* part;                    // (K, DU_PART, 2) partial sums / counts of positives
     float* thr_out;                 // [K] packbits threshold min(mean, thr)
     uint64_t seed;
     int K, C, G, M;
+    int all;                        // warm-up: every cell drawn
     float thr, decay, scale;
 };
 #define DU_PART 512
@@ -411,14 +401,12 @@ k_du_scan(int32_t* __restrict__ v, int nb) {
     if (t == 1023) v[nb] = sPart[1023];
 }
 
-// draws of cell j of segment seg (the occupied part needs the segment's count)
-__device__ __forceinline__ uint32_t du_draws(const DensityUpd& u, int64_t seg, uint32_t j,
-                                             bool occupied, float lam_o) {
-    const uint32_t n0 = du_poisson(0.25f, du_hash(u.seed, (uint32_t)seg, j, 0), 0u);   // M / G^3
-    const uint32_t n1 = occupied ? du_poisson(lam_o, du_hash(u.seed, (uint32_t)seg, j, 1),
-                                              du_hash(u.seed, (uint32_t)seg, j, 5))
-                                 : 0u;
-    return min(n0 + n1, (uint32_t)DU_DUP_MAX);
+// is cell j of segment seg drawn (uniform or occupied draws; the occupied
+// rate needs the segment's count)?
+__device__ __forceinline__ bool du_drawn(const DensityUpd& u, int64_t seg, uint32_t j,
+                                         bool occupied, float lam_o) {
+    return u.all || du_hit(0.25f, du_hash(u.seed, (uint32_t)seg, j, 0)) ||             // M / G^3
+           (occupied && du_hit(lam_o, du_hash(u.seed, (uint32_t)seg, j, 1)));  // M / n_occupied
 }
 
 __device__ __forceinline__ float du_lam_occ(const DensityUpd& u, int64_t seg, int64_t seg_blocks) {
@@ -426,8 +414,8 @@ __device__ __forceinline__ float du_lam_occ(const DensityUpd& u, int64_t seg, in
     return no > 0 ? (float)u.M / (float)no : 0.f;
 }
 
-// 3. per-block count of draws.  MODE 0: counts -> dblk; MODE 1: the ordered
-// list (each lane writes its cell's draws at its prefix position)
+// 3. per-block count of drawn cells.  MODE 0: counts -> dblk; MODE 1: the
+// ordered list (each lane writes its cell at its prefix position)
 template <int MODE>
 __global__ void __launch_bounds__(256)
 k_du_draws(DensityUpd u, int64_t cap) {
@@ -442,7 +430,7 @@ k_du_draws(DensityUpd u, int64_t cap) {
     int total = 0;
     for (int j = 0; j < DU_BLK; j += blockDim.x) {
         const uint32_t cell = (uint32_t)(j0 + j + threadIdx.x);
-        const int n = (int)du_draws(u, seg, cell, g[j + threadIdx.x] > u.thr, lam_o);
+        const int n = du_drawn(u, seg, cell, g[j + threadIdx.x] > u.thr, lam_o) ? 1 : 0;
         if (MODE == 0) { total += n; continue; }
         const int incl = rn_wave_incl_sum_i(n);
         const int w = threadIdx.x / RN_WAVE;
@@ -452,9 +440,7 @@ k_du_draws(DensityUpd u, int64_t cap) {
         for (int q = 0; q < w; ++q) before += sWave[q];
         const int tot = sWave[0] + sWave[1] + sWave[2] + sWave[3];
         const int64_t p0 = base + before + incl - n;
-        for (int d = 0; d < n; ++d)
-            if (p0 + d < cap)
-                u.list[p0 + d] = cell | ((uint32_t)d << 21) | ((uint32_t)c << 26);
+        if (n && p0 < cap) u.list[p0] = cell | ((uint32_t)c << 26);
         base += tot;
         __syncthreads();
     }
@@ -469,8 +455,8 @@ k_du_draws(DensityUpd u, int64_t cap) {
     }
 }
 
-// 4. the listed draws of sub-NeRF k (blockIdx.y), in cell order: jitter,
-// sigma (grid + geo MLP, as k_field_density), scatter-max per cell
+// 4. the drawn cells of sub-NeRF k (blockIdx.y), in cell order: jitter,
+// sigma (grid + geo MLP, as k_field_density), tmp[cell] = sigma
 __global__ void __launch_bounds__(256)
 k_du_sample(FieldArgs a, DensityUpd u, int64_t cap) {
     __shared__ __attribute__((aligned(16))) rn_half sW[8 * RN_FRAG_HALFS];
@@ -493,7 +479,7 @@ k_du_sample(FieldArgs a, DensityUpd u, int64_t cap) {
         const int64_t q = tile * 32 + cl;
         const bool valid = q < n;
         const uint32_t e = valid ? u.list[lo + q] : 0u;
-        const uint32_t cell = e & 0x1fffffu, d = (e >> 21) & 31u;
+        const uint32_t cell = e & 0x1fffffu;
         const int c = (int)(e >> 26);
         const int seg = k * u.C + c;
         // networks.py:386-391: cell centre of cascade c, jittered by +-half a cell
@@ -502,7 +488,7 @@ k_du_sample(FieldArgs a, DensityUpd u, int64_t cap) {
         const float gm1 = (float)(u.G - 1);
         const float cx = (float)rn_morton3d_invert(cell), cy = (float)rn_morton3d_invert(cell >> 1),
                     cz = (float)rn_morton3d_invert(cell >> 2);
-        const uint32_t di = (cell << 5) | d;
+        const uint32_t di = cell << 5;                 // the cell's first draw
         const float jx = du_unit(du_hash(u.seed, seg, di, 2)), jy = du_unit(du_hash(u.seed, seg, di, 3)),
                     jz = du_unit(du_hash(u.seed, seg, di, 4));
         const float x = ((cx / gm1) * 2.0f - 1.0f) * (sc - hgs) + (jx * 2.0f - 1.0f) * hgs;
@@ -522,12 +508,7 @@ k_du_sample(FieldArgs a, DensityUpd u, int64_t cap) {
         f32x16 gg = rn_zero16();
 #pragma unroll
         for (int qq = 0; qq < 4; ++qq) gg = rn_mfma(rn_frag(sW, 4 + qq), h1[qq], gg);
-        if (valid && h == 0) {
-            // duplicate draws of a cell keep their max (deterministic, as rn_scatter_max)
-            const float sig = expf(gg[8]);
-            atomicMax(reinterpret_cast<int*>(u.tmp) + (int64_t)seg * G3 + cell,
-                      __float_as_int(fmaxf(sig, 0.0f)));
-        }
+        if (valid && h == 0) u.tmp[(int64_t)seg * G3 + cell] = expf(gg[8]);   // one per cell
     }
 }
 
@@ -639,7 +620,7 @@ int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, 
                               const uint32_t* level_hsize, const uint32_t* level_res,
                               const float* level_scale, const float* xyz_min, const float* extent,
                               const void* frags, float* tmp, int32_t* occ, int32_t* blk,
-                              float* part, float* thr_out, void* stream) {
+                              float* part, float* thr_out, int32_t all_cells, void* stream) {
     RN_CHECK_ARG(n_models >= 1 && cascades >= 1 && cascades <= 32 && grid_size == 128,
                  "bad sizes (grid_size 128, cascades <= 32)");
     RN_CHECK_ARG(grid_ptrs && bitfield_ptrs && grid_f16 && level_offset && level_hsize &&
@@ -658,6 +639,7 @@ int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, 
     u.seed = seed; u.K = n_models; u.C = cascades; u.G = grid_size;
     u.M = (int)(G3 / 4);                                  // networks.py:378: grid_size**3 // 4
     u.thr = density_threshold; u.decay = decay; u.scale = scale;
+    u.all = all_cells != 0;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(tmp, 0, sizeof(float) * n_all, st) != hipSuccess) {
         rn_set_error("%s: memset failed", __func__);
@@ -668,9 +650,9 @@ int rn_density_update_sampled(const void* grid_ptrs, const void* bitfield_ptrs, 
     k_du_draws<0><<<nb, 256, 0, st>>>(u, n_all);
     k_du_scan<<<1, 1024, 0, st>>>(u.dblk, nb);
     k_du_draws<1><<<nb, 256, 0, st>>>(u, n_all);
-    // expected draws: 2 M per (sub-NeRF, cascade); the kernel strides over
-    // whatever the device-side count is
-    const int64_t tiles = (2 * (int64_t)u.M * cascades + 31) / 32;
+    // drawn cells: at most 2 M per (sub-NeRF, cascade) on average (1 - e^-1/4
+    // of G^3 plus the occupied ones); the kernel strides over the device count
+    const int64_t tiles = ((all_cells ? G3 : 2 * (int64_t)u.M) * cascades + 31) / 32;
     const int sb = (int)(tiles / 4 + 1 < 2048 ? tiles / 4 + 1 : 2048);
     k_du_sample<<<dim3(sb, n_models), 256, 0, st>>>(a, u, n_all);
     k_du_decay<<<dim3(DU_PART, n_models), 256, 0, st>>>(u);

@@ -65,7 +65,10 @@ inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 extern "C" {
 
-int rn_version(void) { return 1; }
+// 2 (round 4): rn_field_bwd_merged takes the page pool of fx_mode 4 (binned
+// scatter) and its 384-B statistics block is named fx_stats; rn_grid_bin /
+// rn_grid_sum / rn_grid_binned_fold added
+int rn_version(void) { return RN_ABI_VERSION; }
 
 const char* rn_last_error(void) { return g_err; }
 

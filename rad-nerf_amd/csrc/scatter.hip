@@ -1,0 +1,278 @@
+// Binned grid-gradient scatter, passes 2 and 3 (the merged backward's walk,
+// field.hip GM 4, is pass 1: it appends each level's records to pages).
+//
+//   k_grid_bin  one workgroup per page: counting sort of the page's records
+//               by slice (GB_SLICE entries of the page's level) in LDS, the
+//               sorted page written back coalesced, plus each slice's run
+//               (start, count) and the page's entry in its level's page list;
+//   k_grid_sum  one workgroup per slice: the slice's runs of every page of
+//               its level added into an int64 copy of the slice in LDS
+//               (ds_add_u64: exact and order-free), then
+//               grid_grad += acc * 2^-e_l once per touched entry.
+//
+// Both passes move 8 B per record with full-line accesses (pages of 64 KB,
+// runs of ~128 records at C5), against the 64-B memory-side request per
+// 1.84 records of the atomic form.  See rn_bin.h for the formats.
+// Reference: the tcnn grid-encoding backward (hash-grid parameter gradient)
+// behind /root/reference/models/networks.py:300-328.
+#include "rn_common.h"
+#include "rn_field.h"
+#include "rn_bin.h"
+
+namespace {
+
+#define GB_BIN_THREADS 256
+#define GB_SUM_THREADS 1024
+#define GB_PER_THREAD (GB_PAGE / GB_BIN_THREADS)
+
+__global__ void __launch_bounds__(GB_BIN_THREADS)
+k_grid_bin(GbPool P) {
+    __shared__ uint64_t sRec[GB_PAGE];
+    __shared__ uint32_t sHist[GB_MAX_BINS];
+    const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
+    const uint32_t np = min(__builtin_nontemporal_load(&P.ctl->pool_next), P.pool_pages);
+    for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
+        const uint32_t meta = P.page_meta[p];
+        const uint32_t l = meta & 31u, n = meta >> 8;
+        for (int i = tid; i < GB_MAX_BINS; i += GB_BIN_THREADS) sHist[i] = 0u;
+        __syncthreads();
+        const uint64_t* src = P.pages_in + (size_t)p * GB_PAGE;
+        uint64_t r[GB_PER_THREAD];
+        uint32_t key[GB_PER_THREAD];
+#pragma unroll
+        for (int j = 0; j < GB_PER_THREAD; ++j) {
+            const uint32_t i = tid + GB_BIN_THREADS * j;
+            r[j] = i < n ? __builtin_nontemporal_load(src + i) : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < GB_PER_THREAD; ++j) {
+            const uint32_t i = tid + GB_BIN_THREADS * j;
+            if (i < n) {
+                const uint32_t b = gb_idx(r[j]) >> GB_SLICE_BITS;
+                key[j] = (b << 16) | atomicAdd(&sHist[b], 1u);
+            }
+        }
+        __syncthreads();
+        if (wid == 0) {                 // exclusive scan of the bins, GB_BPL per lane
+            constexpr int GB_BPL = GB_MAX_BINS / 64;
+            uint32_t h[GB_BPL], tot = 0u;
+#pragma unroll
+            for (int k = 0; k < GB_BPL; ++k) { h[k] = sHist[GB_BPL * lane + k]; tot += h[k]; }
+            uint32_t incl = tot;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
+                incl += lane >= off ? o : 0u;
+            }
+            uint32_t s0 = incl - tot;
+            uint32_t* d = P.desc + (size_t)p * GB_MAX_BINS;
+#pragma unroll
+            for (int k = 0; k < GB_BPL; ++k) {
+                d[GB_BPL * lane + k] = s0 | (h[k] << 16);
+                sHist[GB_BPL * lane + k] = s0;
+                s0 += h[k];
+            }
+            if (lane == 0 && n > 0) {
+                const uint32_t slot = atomicAdd(&P.ctl->level_npages[l], 1u);
+                P.level_pages[(size_t)l * P.pool_pages + slot] = p;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < GB_PER_THREAD; ++j) {
+            const uint32_t i = tid + GB_BIN_THREADS * j;
+            if (i < n) sRec[sHist[key[j] >> 16] + (key[j] & 0xffffu)] = r[j];
+        }
+        __syncthreads();
+        uint64_t* dst = P.pages_out + (size_t)p * GB_PAGE;
+#pragma unroll 4
+        for (uint32_t i = tid; i < n; i += GB_BIN_THREADS) __builtin_nontemporal_store(sRec[i], dst + i);
+    }
+}
+
+struct GbSumArgs {
+    uint32_t first[RN_L + 1];     // first slice of the q-th level in launch order (level 15 - q)
+    uint32_t off[RN_L], hs[RN_L];
+};
+
+// ABL (timing studies only, tools/bin_probe.py): 1 no LDS adds (records
+// XOR-folded into a register), 2 int32 LDS adds instead of int64
+template <int ABL>
+__device__ __forceinline__ void gb_add(int64_t* acc, uint64_t r, uint64_t& fold) {
+    const uint32_t e = gb_idx(r) & (GB_SLICE - 1u);
+    if (ABL == 1) {
+        fold ^= r;
+    } else if (ABL == 2) {
+        int32_t* a32 = reinterpret_cast<int32_t*>(acc);
+        __hip_atomic_fetch_add(a32 + 2 * e, (int32_t)gb_v0(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(a32 + 2 * e + 1, (int32_t)gb_v1(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    } else {
+        __hip_atomic_fetch_add(acc + 2 * e, gb_v0(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(acc + 2 * e + 1, gb_v1(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+#define GB_RUNS 16                // runs of one wave in flight
+
+template <int ABL, int RUNS = GB_RUNS, bool NT = true>
+__global__ void __launch_bounds__(GB_SUM_THREADS, 8)   // two workgroups per CU
+k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t* __restrict__ redo,
+           float* __restrict__ grad) {
+    extern __shared__ int64_t acc[];               // [GB_SLICE][2]
+    if (redo && __builtin_nontemporal_load(redo) != 0) return;   // the fp32 redo replaces the step
+    int q = 0;
+#pragma unroll
+    for (int k = 1; k < RN_L; ++k) q = blockIdx.x >= s.first[k] ? k : q;
+    const int l = RN_L - 1 - q;
+    const uint32_t b = blockIdx.x - s.first[q];
+    const uint32_t npg = min(__builtin_nontemporal_load(&P.ctl->level_npages[l]), P.pool_pages);
+    const float sc = scale[l];
+    if (npg == 0u || sc == 0.f) return;            // no records (an fp32 level went in by atomics)
+    const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
+    for (int i = tid; i < 2 * (int)GB_SLICE; i += GB_SUM_THREADS) acc[i] = 0;
+    __syncthreads();
+    const uint32_t* lp = P.level_pages + (size_t)l * P.pool_pages;
+    constexpr uint32_t NW = GB_SUM_THREADS / RN_WAVE;
+    // lane i of a wave holds page base + i's run of this slice (page, start |
+    // count << 16); the next batch's runs are loaded while this one is summed
+    auto runs_of = [&](uint32_t base, uint32_t& pg, uint32_t& d) {
+        const uint32_t i = base + lane;
+        pg = 0u; d = 0u;
+        if (i < npg) {
+            pg = lp[i];
+            d = P.desc[(size_t)pg * GB_MAX_BINS + b];
+        }
+    };
+    uint32_t pg, d;
+    uint64_t fold = 0ull;
+    runs_of(wid * 64u, pg, d);
+    for (uint32_t base = wid * 64u; base < npg; base += NW * 64u) {
+        const uint32_t pgc = pg, dc = d;
+        runs_of(base + NW * 64u, pg, d);
+#pragma unroll 1
+        for (int k0 = 0; k0 < 64; k0 += RUNS) {
+            uint64_t r[RUNS];
+            uint32_t cnt[RUNS];
+#pragma unroll
+            for (int j = 0; j < RUNS; ++j) {
+                const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
+                const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
+                cnt[j] = dk >> 16;
+                const uint64_t* run = P.pages_out + (size_t)pk * GB_PAGE + (dk & 0xffffu);
+                r[j] = (uint32_t)lane < cnt[j] ? (NT ? __builtin_nontemporal_load(run + lane) : run[lane])
+                                               : 0ull;
+            }
+#pragma unroll
+            for (int j = 0; j < RUNS; ++j) {
+                if ((uint32_t)lane < cnt[j]) gb_add<ABL>(acc, r[j], fold);
+                if (cnt[j] > 64u) {                // the rest of a longer run (uniform branch)
+                    const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
+                    const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
+                    const uint64_t* run = P.pages_out + (size_t)pk * GB_PAGE + (dk & 0xffffu);
+                    for (uint32_t o = 64u + lane; o < cnt[j]; o += 64u)
+                        gb_add<ABL>(acc, __builtin_nontemporal_load(run + o), fold);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (ABL == 1 && fold == 0x0123456789abcdefull) acc[0] = 1;    // keeps the loads
+    const float inv = 1.0f / sc;                   // exact: a power of two
+    const uint32_t e0 = b * GB_SLICE;
+    const uint32_t ne = min(GB_SLICE, s.hs[l] - e0);
+    float2* g = reinterpret_cast<float2*>(grad) + (size_t)s.off[l] + e0;
+    for (uint32_t e = tid; e < ne; e += GB_SUM_THREADS) {
+        const int64_t a0 = acc[2 * e], a1 = acc[2 * e + 1];
+        if ((a0 | a1) == 0) continue;
+        float2 v = g[e];
+        v.x += (float)a0 * inv;
+        v.y += (float)a1 * inv;
+        g[e] = v;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int rn_grid_bin_layout(int32_t* out) {
+    RN_CHECK_ARG(out, "null pointer");
+    out[0] = GB_PAGE; out[1] = GB_MAX_BINS; out[2] = (int32_t)GB_SLICE;
+    out[3] = (int32_t)sizeof(GbCtl); out[4] = GB_IDX_BITS; out[5] = GB_V_BITS;
+    return 0;
+}
+
+int rn_grid_bin(void* ctl, const uint32_t* page_meta, const uint64_t* pages_in,
+                uint64_t* pages_out, uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
+                int32_t blocks, void* stream) {
+    RN_CHECK_ARG(ctl && page_meta && pages_in && pages_out && desc && level_pages, "null pointer");
+    RN_CHECK_ARG(pool_pages >= 1 && blocks >= 1, "bad sizes");
+    GbPool P{};
+    P.ctl = (GbCtl*)ctl; P.page_meta = (uint32_t*)page_meta; P.pages_in = (uint64_t*)pages_in;
+    P.pages_out = pages_out; P.desc = desc; P.level_pages = level_pages;
+    P.pool_pages = (uint32_t)pool_pages;
+    k_grid_bin<<<blocks, GB_BIN_THREADS, 0, (hipStream_t)stream>>>(P);
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const void* ctl,
+                const uint32_t* desc, const uint32_t* level_pages, const uint64_t* pages_out,
+                int32_t pool_pages, const float* fx_scale, const int32_t* redo, float* grid_grad,
+                void* stream) {
+    RN_CHECK_ARG(level_offset && level_hsize && ctl && desc && level_pages && pages_out &&
+                 fx_scale && grid_grad, "null pointer");
+    RN_CHECK_ARG(pool_pages >= 1, "bad sizes");
+    GbSumArgs s{};
+    uint32_t total = 0;
+    for (int q = 0; q < RN_L; ++q) {            // the finest (heaviest) levels first
+        const int l = RN_L - 1 - q;
+        RN_CHECK_ARG(level_hsize[l] <= (GB_MAX_BINS << GB_SLICE_BITS) &&
+                         level_hsize[l] <= (1u << GB_IDX_BITS), "level too large for binning");
+        s.first[q] = total;
+        total += (level_hsize[l] + GB_SLICE - 1) / GB_SLICE;
+    }
+    s.first[RN_L] = total;
+    for (int l = 0; l < RN_L; ++l) { s.off[l] = level_offset[l]; s.hs[l] = level_hsize[l]; }
+    GbPool P{};
+    P.ctl = (GbCtl*)ctl; P.desc = (uint32_t*)desc; P.level_pages = (uint32_t*)level_pages;
+    P.pages_out = (uint64_t*)pages_out; P.pool_pages = (uint32_t)pool_pages;
+    const size_t lds = (size_t)GB_SLICE * 2 * sizeof(int64_t);
+    // ablations (timing studies only): bits 16-17 ABL, bit 18 plain loads,
+    // bit 19 32 runs in flight per wave
+    const int dbg = rn_debug_flags_internal() >> 16;
+    const int abl = dbg & 3;
+    hipStream_t st = (hipStream_t)stream;
+#define GB_SUM_LAUNCH(A, R, N) \
+    k_grid_sum<A, R, N><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad)
+    if (dbg == 0) GB_SUM_LAUNCH(0, GB_RUNS, true);
+    else if (abl == 1 && (dbg & 4)) GB_SUM_LAUNCH(1, GB_RUNS, false);
+    else if (abl == 1 && (dbg & 8)) GB_SUM_LAUNCH(1, 32, true);
+    else if (abl == 1) GB_SUM_LAUNCH(1, GB_RUNS, true);
+    else if (abl == 2) GB_SUM_LAUNCH(2, GB_RUNS, true);
+    else if (dbg & 4) GB_SUM_LAUNCH(0, GB_RUNS, false);
+    else if (dbg & 8) GB_SUM_LAUNCH(0, 32, true);
+    else GB_SUM_LAUNCH(0, GB_RUNS, true);
+#undef GB_SUM_LAUNCH
+    RN_CHECK_LAUNCH();
+    return 0;
+}
+
+int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsize, void* ctl,
+                        const uint32_t* page_meta, const uint64_t* pages_in, uint64_t* pages_out,
+                        uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
+                        const float* fx_scale_cur, float* fx_scale_next, uint32_t* fx_stats,
+                        int32_t* fx_redo, float* grid_grad, void* stream) {
+    RN_CHECK_ARG(fx_scale_cur && fx_scale_next && fx_stats && fx_redo, "null pointer");
+    RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
+    int st = rn_grid_bin(ctl, page_meta, pages_in, pages_out, desc, level_pages, pool_pages,
+                         2048, stream);
+    if (st) return st;
+    st = rn_fx_check_binned(fx_scale_cur, fx_scale_next, fx_stats, fx_redo, ctl,
+                            (uint32_t)pool_pages, stream);
+    if (st) return st;
+    return rn_grid_sum(level_offset, level_hsize, ctl, desc, level_pages, pages_out, pool_pages,
+                       fx_scale_cur, fx_redo, grid_grad, stream);
+}
+
+}  // extern "C"

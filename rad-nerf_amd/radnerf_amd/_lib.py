@@ -31,7 +31,7 @@ SIGNATURES = {
     "rn_debug_cycles": [P],
     "rn_set_level_pairing": [ctypes.c_uint64],
     "rn_density_update_sampled": [P, P, I32, I32, I32, F32, F32, F32, U64, P, P, P, P, P, P, P,
-                                  P, P, P, P, P, P, P],
+                                  P, P, P, P, P, P, I32, P],
     "rn_distortion_loss_fw": [P, P, P, P, I64, P, P, P, P],
     "rn_distortion_loss_bw": [P, P, P, P, P, P, P, I64, P, P],
     "rn_raymarching_train_count": [P, P, P, P, I32, F32, F32, P, I32, I32, I64, P, P],
@@ -57,8 +57,12 @@ SIGNATURES = {
     "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
                             P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P, P, P,
-                            P, I32, P],
+                            P, I32, P, P, P, I32, P],
     "rn_grid_fx_fold": [P, P, P, P, P, P, P, P, P, P],
+    "rn_grid_bin_layout": [P],
+    "rn_grid_bin": [P, P, P, P, P, P, I32, I32, P],
+    "rn_grid_sum": [P, P, P, P, P, P, I32, P, P, P, P],
+    "rn_grid_binned_fold": [P, P, P, P, P, P, P, P, I32, P, P, P, P, P, P],
     "rn_render_test": [P, P, P, I64, I32, P, I64, I32, F32, F32, I32, I32, P, P, P, P, P, P, P,
                        P, F32, P, P, P, P, I32, P],
     "rn_seed_scale": [P, P, I32, P, P, P, P, P, P],
@@ -80,6 +84,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
+ABI_VERSION = 2
 _lib = None
 
 
@@ -120,12 +125,29 @@ class _Lib:
     def version(self):
         return self.handle.rn_version()
 
+    def bin_layout(self):
+        """the binned scatter's page layout (csrc/rn_bin.h, rn_grid_bin_layout)"""
+        if getattr(self, "_bin_layout", None) is None:
+            out = (ctypes.c_int32 * 6)()
+            self.grid_bin_layout(out)
+            self._bin_layout = dict(page=out[0], bins=out[1], slice=out[2], ctl_bytes=out[3],
+                                    idx_bits=out[4], v_bits=out[5])
+        return self._bin_layout
+
+    def check_version(self):
+        """the ABI this binding was written against (include/radnerf.h RN_ABI_VERSION)"""
+        v = self.version()
+        if v != ABI_VERSION:
+            raise ImportError(f"radnerf_amd: librn.so ABI {v}, binding expects {ABI_VERSION}; "
+                              f"rebuild with `make -C rad-nerf_amd/csrc`")
+
 
 def lib():
     """The loaded librn.so (raises ImportError when it is missing)."""
     global _lib
     if _lib is None:
         _lib = _Lib(LIB_PATH)
+        _lib.check_version()
     return _lib
 
 

@@ -66,6 +66,7 @@ class GradAllReduce:
 
     def __init__(self, params, device):
         self.params = list(params)
+        self.timed = []                 # finished launch_range handles (comm_stats)
         sizes = [p.numel() for p in self.params]
         self.flat = torch.zeros(sum(sizes), device=device)
         self.views = []
@@ -99,6 +100,97 @@ class GradAllReduce:
         """Asynchronous SUM all-reduce of every bucket; [(range, work)]."""
         return [((a, b), dist.all_reduce(self.flat[a:b], async_op=True))
                 for a, b in self._ranges(n_buckets)]
+
+    # ---- staged launches with per-bucket timing (bench.py's comm fields) ----
+    def param_range(self, first, last=None):
+        """[a, b) of the flat buffer spanning params[first:last]."""
+        sizes = [p.numel() for p in self.params]
+        last = len(sizes) if last is None else last
+        return sum(sizes[:first]), sum(sizes[:last])
+
+    def launch_range(self, a, b, n_buckets=1):
+        """Start SUM all-reduces of flat[a:b] in n_buckets pieces as soon as the
+        compute stream has produced them: on a comm stream that waits for the
+        compute stream, bracketed by events there (CUDA), so the collectives
+        overlap whatever the compute stream does next.  Returns a handle for
+        finish(); a no-op with one rank."""
+        if not (dist.is_initialized() and dist.get_world_size() > 1):
+            return None
+        n = b - a
+        n_buckets = max(1, min(int(n_buckets), max(1, n // 64)))
+        bounds = [a + (n * i // n_buckets) // 64 * 64 for i in range(n_buckets)] + [b]
+        cuda = self.flat.is_cuda
+        handle = {"parts": [], "cuda": cuda}
+        if cuda:
+            main = torch.cuda.current_stream(self.flat.device)
+            if getattr(self, "_comm", None) is None:
+                self._comm = torch.cuda.Stream(self.flat.device)
+            comm = self._comm
+            comm.wait_stream(main)
+            handle["stream"] = comm
+            with torch.cuda.stream(comm):
+                for lo, hi in zip(bounds[:-1], bounds[1:]):
+                    if hi <= lo:
+                        continue
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(comm)
+                    w = dist.all_reduce(self.flat[lo:hi], async_op=True)
+                    w.wait()                  # the comm stream waits for the collective
+                    e1.record(comm)
+                    handle["parts"].append(((lo, hi), e0, e1))
+        else:
+            import time
+            for lo, hi in zip(bounds[:-1], bounds[1:]):
+                if hi <= lo:
+                    continue
+                t0 = time.perf_counter()
+                w = dist.all_reduce(self.flat[lo:hi], async_op=True)
+                handle["parts"].append(((lo, hi), w, t0))
+        return handle
+
+    def finish(self, handle, average=True):
+        """Join a launch_range handle into the compute stream and average."""
+        if handle is None:
+            return
+        world = dist.get_world_size()
+        if handle["cuda"]:
+            torch.cuda.current_stream(self.flat.device).wait_stream(handle["stream"])
+            parts = handle["parts"]
+        else:
+            import time
+            parts = []
+            for rng, w, t0 in handle["parts"]:
+                w.wait()
+                parts.append((rng, t0, time.perf_counter()))
+            handle["parts"] = parts
+        if average:
+            for (lo, hi), _, _ in parts:
+                self.flat[lo:hi].div_(world)
+        self.timed.append(handle)
+
+    def comm_stats(self, steps):
+        """Per-step collective figures of the handles finished since
+        reset_timing(): allreduce_ms (sum of the buckets' durations on the
+        comm stream), buckets per step, bytes per rank (payload and a ring
+        all-reduce's 2 (P-1)/P of it).  Synchronises."""
+        world = dist.get_world_size() if dist.is_initialized() else 1
+        tot, n_parts, payload = 0.0, 0, 0
+        for h in self.timed:
+            for (lo, hi), a, b in h["parts"]:
+                if h["cuda"]:
+                    a.synchronize(); b.synchronize()
+                    tot += a.elapsed_time(b)
+                else:
+                    tot += (b - a) * 1e3
+                n_parts += 1
+                payload += (hi - lo) * self.flat.element_size()
+        steps = max(1, int(steps))
+        return {"allreduce_ms": round(tot / steps, 4), "buckets_per_step": n_parts / steps,
+                "bytes_per_rank": int(payload / steps),
+                "ring_bytes_per_rank": int(payload / steps * 2 * (world - 1) / max(world, 1))}
+
+    def reset_timing(self):
+        self.timed = []
 
     def reduce(self, average=True, n_buckets=1):
         """All-reduce the flat gradient as n_buckets asynchronous collectives;

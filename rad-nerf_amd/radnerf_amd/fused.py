@@ -23,6 +23,7 @@ from ._lib import lib
 MAX_SAMPLES = 1024
 NEAR_DISTANCE = 0.01
 SEG_ALIGN = 128
+FX_STATS_BYTES = 640      # include/radnerf.h RN_FX_STATS_BYTES
 
 
 def _stream(dev):
@@ -89,14 +90,37 @@ class Workspace:
         """Fixed-point grid-gradient state (rn_grid_fx_fold): int32 sums (n,
         zero between steps), per-level scales (2, 16) (current / next, swapped
         by fx_i each step; zeros = fp32 until the first step has measured the
-        records), the per-level statistics block (384 B: record maxima, record
-        sums, entry sums; include/radnerf.h) and the redo flag."""
+        records), the per-level statistics block (FX_STATS_BYTES: record
+        maxima, plain and weighted record / entry sums; include/radnerf.h)
+        and the redo flag."""
         if getattr(self, "_fx", None) is None or self._fx[0].numel() != n:
             z = dict(device=device, dtype=torch.int32)
             self._fx = (torch.zeros(n, **z), torch.zeros(2, 16, device=device),
-                        torch.zeros(96, **z), torch.zeros(1, **z))
+                        torch.zeros(FX_STATS_BYTES // 4, **z), torch.zeros(1, **z))
             self.fx_i = 0
         return self._fx
+
+    def bin_pool(self, pages):
+        """Page pool of the binned grid-gradient scatter (fx_mode 4,
+        rn_grid_binned_fold; csrc/rn_bin.h): control block, page levels /
+        fills, the pages (u64 records; the bin pass sorts each page in place),
+        per-page slice runs, per-level page lists, and a pinned word that
+        receives the pages the last backward took (read without a sync: the
+        pool grows for later steps; a step that overflows is redone in fp32)."""
+        b = getattr(self, "_bin", None)
+        if b is None or b["pages"] < pages:
+            lay = lib().bin_layout()
+            i = dict(device=self.device, dtype=torch.int32)
+            self._bin = b = dict(
+                pages=pages, page=lay["page"],
+                ctl=torch.zeros(lay["ctl_bytes"] // 4, **i),
+                meta=torch.zeros(pages, **i),
+                recs=torch.empty(pages * lay["page"], device=self.device, dtype=torch.int64),
+                desc=torch.empty(pages * lay["bins"], **i),
+                lpages=torch.empty(16 * pages, **i),
+                seen=torch.zeros(1, dtype=torch.int32, pin_memory=True),
+                seen_ev=None)
+        return b
 
     def bwd_scratch(self, blocks, max_chunk, max_samples=MAX_SAMPLES):
         """Per-block row scratch and dW park area of rn_field_bwd_merged."""
@@ -208,6 +232,16 @@ class FusedMLRenderer:
         # from C2's 8192 rays on fixed point does (C2 800 vs 696, C3 1078 vs
         # 998; tools/gpu/fx_small.sh, profiles/r03/fx_small_r03.jsonl)
         self.grid_fx = rk > 1024
+        # binned ("store and sum") scatter of the fixed-point records at scale
+        # 16 (fx_mode 4 + rn_grid_binned_fold): the walk appends records to
+        # pages with plain stores, a bin pass sorts each page by 4096-entry
+        # slice, a sum pass adds each slice in LDS (int64, exact) -- instead
+        # of memory-side atomics, which were 45 % of C5's field_bwd
+        # (DESIGN §4 "Binned scatter")
+        self.grid_bin = self.grid_fx and float(model.scale) > 0.5
+        # initial pool: records per (ray, sub-NeRF) at scale 16 (C5's replay:
+        # 63.5 records x 95 samples; tools/records_sim.py), x 1.15
+        self.bin_records_per_pair = 6912
         self.min_chunk = 512
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
@@ -224,6 +258,9 @@ class FusedMLRenderer:
         # input gradients (dL/drays_o, dL/drays_d) in backward(): set by
         # _MLRenderFn when the rays require grad (--optimize_ext)
         self.input_grad = False
+        # called right after the merged field_bwd launch (stream order), when
+        # the MLP gradient is final (data-parallel early all-reduce)
+        self.after_field_bwd = None
         # record HIP events around every launch (True) or the named ones (a set)
         self.trace = False
         self.events = {}
@@ -384,11 +421,18 @@ class FusedMLRenderer:
             chunks = self._chunks
             ig = (None, None, None)
             fx = (None, None, None, None, 0)
+            gb = (None, None, None, 0)
             use_fx = self.grid_fx and self.feat_cache and not self.int_grad
+            use_bin = use_fx and self.grid_bin
             if use_fx:
-                acc, scales, vmax, redo = w.fx_buffers(grid_grad.numel(), grid_grad.device)
+                acc, scales, stats, redo = w.fx_buffers(grid_grad.numel(), grid_grad.device)
                 cur, nxt = scales[w.fx_i], scales[1 - w.fx_i]
-                fx = (acc.data_ptr(), cur.data_ptr(), vmax.data_ptr(), None, 2)
+                fx = (acc.data_ptr(), cur.data_ptr(), stats.data_ptr(), None, 2)
+            if use_bin:
+                pool = self._bin_pool(w)
+                fx = (None, cur.data_ptr(), stats.data_ptr(), None, 4)
+                gb = (pool["ctl"].data_ptr(), pool["meta"].data_ptr(), pool["recs"].data_ptr(),
+                      pool["pages"])
             if self.int_grad:
                 n_g = grid_grad.numel()
                 if getattr(w, "_igrad", None) is None or w._igrad[0].numel() != n_g:
@@ -409,13 +453,31 @@ class FusedMLRenderer:
                      *common[10:], w.dsigma.data_ptr(), w.drgb.data_ptr(), grid_grad.data_ptr(),
                      dw.data_ptr(), w.feat.data_ptr() if self.feat_cache else None,
                      scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
-                     self.merged_blocks, *ig, *fx, st)
-            if use_fx:
+                     self.merged_blocks, *ig, *fx, *gb, st)
+            if self.after_field_bwd is not None:
+                # the MLP gradient (dW) is final here; the grid gradient only
+                # after the fold / bin + sum below: a data-parallel caller
+                # starts the MLP / gate all-reduce now (bench.py)
+                self.after_field_bwd()
+            if use_bin:
+                # bin + sum the pages into grid_grad (or flag the step for the
+                # fp32 redo: a record past the int22 range, a pool overflow)
+                self._ev("fx_fold", L.grid_binned_fold, lo, lh, pool["ctl"].data_ptr(),
+                         pool["meta"].data_ptr(), pool["recs"].data_ptr(),
+                         pool["recs"].data_ptr(), pool["desc"].data_ptr(),
+                         pool["lpages"].data_ptr(), pool["pages"], cur.data_ptr(),
+                         nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(),
+                         grid_grad.data_ptr(), st)
+                pool["seen"].copy_(pool["ctl"][:1], non_blocking=True)
+                pool["seen_ev"] = torch.cuda.Event()
+                pool["seen_ev"].record(torch.cuda.current_stream(grid_grad.device))
+            elif use_fx:
                 # fold the fixed-point sums into grid_grad (or flag the step for
                 # the fp32 redo), next step's scales; the redo launch exits at
                 # once unless flagged (no host synchronisation either way)
                 self._ev("fx_fold", L.grid_fx_fold, lo, lh, lr, acc.data_ptr(), cur.data_ptr(),
-                         nxt.data_ptr(), vmax.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(), st)
+                         nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(),
+                         st)
                 self._ev("fx_redo", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                          rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                          w.seg_count.data_ptr(), w.mstart.data_ptr(),
@@ -424,7 +486,7 @@ class FusedMLRenderer:
                          grid_grad.data_ptr(), dw.data_ptr(), w.feat.data_ptr(),
                          scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
                          self.merged_blocks, None, None, None, None, cur.data_ptr(), None,
-                         redo.data_ptr(), 3, st)
+                         redo.data_ptr(), 3, None, None, None, 0, st)
                 w.fx_i ^= 1
             if self.int_grad:
                 self._ev("igrad_to_f32", L.igrad_to_f32, grid_grad.numel(), ig[0], ig[1], ig[2],
@@ -433,6 +495,22 @@ class FusedMLRenderer:
             self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
                      w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),
                      w.feat.data_ptr() if self.feat_cache else None, self.bwd_blocks, st)
+
+    def _bin_pool(self, w):
+        """The page pool for this backward, grown when the last binned
+        backward's page count (read back without a sync) came near its size."""
+        lay = lib().bin_layout()
+        b = getattr(w, "_bin", None)
+        if b is None:
+            need = -(-self.bin_records_per_pair * w.B * w.K // lay["page"])
+        else:
+            need = b["pages"]
+            ev = b["seen_ev"]
+            if ev is not None and ev.query():
+                used = int(b["seen"][0])
+                if used * 8 > need * 7:          # above 7/8: grow to 1.5x what was used
+                    need = used * 3 // 2 + 64
+        return w.bin_pool(need)
 
     # ----------------------------------------------------------------- backward
     def backward(self, rays_o, rays_d, gate_in2, gate, bg, dL_drgb, dL_dopacity, dL_ddepth,

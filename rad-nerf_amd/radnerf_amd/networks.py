@@ -17,6 +17,7 @@ Parameters are fp32 masters: `xyz_encoder.params` (hash table, (entries*2,)),
 kernels whenever the master changed (tracked with the tensor version counter).
 tcnn's own flat-parameter ordering is not reproduced (unpinned dependency).
 """
+import functools
 import math
 
 import numpy as np
@@ -339,76 +340,48 @@ class MNGP(nn.Module):
 
     @torch.no_grad()
     def sample_uniform_and_occupied_cells(self, M, density_threshold, ind, generator=None):
-        """networks.py:345-372 (generator: the random stream; None = torch's
-        default, as the reference)"""
-        cells = []
-        density_grid = getattr(self, f"density_grid_{ind}")
+        """networks.py:345-372 as an API: per cascade, (Morton indices, coords)
+        of M uniform cells followed by M cells drawn with replacement among
+        those denser than the threshold (none when no cell is).  The update
+        itself no longer draws explicit cells (rn_density_update_sampled
+        decides per cell whether it is hit, with the same hit rates)."""
+        grid = getattr(self, f"density_grid_{ind}")
+        draw = functools.partial(torch.randint, device=grid.device, generator=generator)
+        out = []
         for c in range(self.cascades):
-            coords1 = torch.randint(self.grid_size, (M, 3), dtype=torch.int32,
-                                    device=density_grid.device, generator=generator)
-            indices1 = vren.morton3D(coords1).long()
-            indices2 = torch.nonzero(density_grid[c] > density_threshold)[:, 0]
-            if len(indices2) > 0:
-                rand_idx = torch.randint(len(indices2), (M,), device=density_grid.device,
-                                         generator=generator)
-                indices2 = indices2[rand_idx]
-                coords2 = vren.morton3D_invert(indices2.int())
-                cells += [(torch.cat([indices1, indices2]), torch.cat([coords1, coords2]))]
-            else:
-                cells += [(indices1, coords1)]
-        return cells
+            coords = draw(self.grid_size, (M, 3), dtype=torch.int32)
+            dense = torch.flatnonzero(grid[c] > density_threshold)
+            if dense.numel():
+                picked = dense[draw(dense.numel(), (M,))].int()
+                coords = torch.cat([coords, vren.morton3D_invert(picked)])
+            out.append((vren.morton3D(coords).long(), coords))
+        return out
 
     @torch.no_grad()
     def update_density_grid(self, density_threshold, warmup=False, decay=0.95, erode=False,
                             generator=None, seed=None):
-        """networks.py:375-409.  With `seed` (an int), the sampled update
-        (warmup False) runs on the device in one call for every sub-NeRF and
-        cascade (rn_density_update_sampled: cell draws from a counter-based
-        hash of the seed, no host synchronisation); radnerf_amd.dist and the
-        Trainer pass the step's seed.  `generator` (a torch.Generator on the model's
-        device) replaces torch's default random stream for the cell draws and
-        the jitter: with ray-batch data parallelism every rank passes one
-        seeded identically (radnerf_amd.dist.update_density_grid), so the
-        ranks draw the same cells and, with identical parameters and
-        deterministic kernels, keep bit-identical grids and bitfields with no
-        collective.  sigma comes from the density-only kernel (rn_field_density:
-        hash grid + geo MLP, networks.py:393-394)."""
-        if seed is not None and not warmup:
-            return self._update_sampled_device(density_threshold, decay, seed)
-        for i in range(self.size):
-            density_grid = getattr(self, f"density_grid_{i}")
-            density_bitfield = getattr(self, f"density_bitfield_{i}")
-            tmp = torch.zeros_like(density_grid)
-            if warmup:
-                cells = self.get_all_cells()
-            else:
-                cells = self.sample_uniform_and_occupied_cells(self.grid_size ** 3 // 4,
-                                                               density_threshold, i, generator)
-            for c in range(self.cascades):
-                indices, coords = cells[c]
-                s = min(2 ** (c - 1), self.scale)
-                half_grid_size = s / self.grid_size
-                xyzs_w = (coords / (self.grid_size - 1) * 2 - 1) * (s - half_grid_size)
-                jitter = torch.rand(xyzs_w.shape, device=xyzs_w.device, generator=generator)
-                xyzs_w += (jitter * 2 - 1) * half_grid_size
-                # duplicate cells (the uniform and the occupied draws overlap):
-                # the reference's index_put keeps an arbitrary one of them
-                # (nondeterministic on the GPU); the max is deterministic, so
-                # ranks with identical inputs keep identical grids
-                sig = self.density(xyzs_w, i)
-                lib().scatter_max(indices.contiguous().data_ptr(), sig.data_ptr(), sig.numel(),
-                                  tmp[c].data_ptr(), _stream(sig.device))
-            density_grid = torch.where(density_grid < 0, density_grid,
-                                       torch.maximum(density_grid * decay, tmp))
-            mean_density = density_grid[density_grid > 0].mean().item()
-            vren.packbits(density_grid.contiguous(), min(mean_density, density_threshold),
-                          density_bitfield)
-            setattr(self, f"density_grid_{i}", density_grid)
+        """networks.py:375-409 on the device, every sub-NeRF and cascade in one
+        rn_density_update_sampled call (warm-up: every cell; otherwise the
+        cells hit by the uniform and the occupied draws, each evaluated once at
+        a jittered point, as the reference's index_put keeps one draw per cell).
+        The draws and jitters come from a counter-based hash of `seed`; without
+        one, the seed is drawn from `generator` (a torch.Generator: ranks that
+        seed it identically keep bit-identical grids and bitfields with no
+        collective, radnerf_amd.dist) or from torch's default generator (as the
+        reference's torch.randint / rand_like).  sigma comes from the density
+        kernel (hash grid + geo MLP, networks.py:393-394).  `erode` (off in
+        train_ml.py) is not supported."""
+        if erode:
+            raise NotImplementedError("update_density_grid(erode=True): not used by train_ml.py")
+        if seed is None:
+            dev = generator.device if generator is not None else torch.device("cpu")
+            seed = int(torch.randint(1 << 62, (1,), generator=generator, device=dev))
+        return self._update_sampled_device(density_threshold, decay, seed, all_cells=warmup)
 
     @torch.no_grad()
-    def _update_sampled_device(self, density_threshold, decay, seed):
-        """The sampled update of every sub-NeRF in one rn_density_update_sampled
-        call; the density grids and bitfields are updated in place."""
+    def _update_sampled_device(self, density_threshold, decay, seed, all_cells=False):
+        """The update of every sub-NeRF in one rn_density_update_sampled call;
+        the density grids and bitfields are updated in place."""
         K, C, G = self.size, self.cascades, self.grid_size
         dev = self.mlp_params.device
         n = K * C * G ** 3
@@ -437,7 +410,7 @@ class MNGP(nn.Module):
             self.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, self._h_min.ctypes.data,
             self._h_ext.ctypes.data, self.packed_frags().data_ptr(), du["tmp"].data_ptr(),
             du["occ"].data_ptr(), du["blk"].data_ptr(), du["part"].data_ptr(),
-            du["thr"].data_ptr(), _stream(dev))
+            du["thr"].data_ptr(), int(bool(all_cells)), _stream(dev))
         self._du_ptrs = ptrs          # keep the pointer array alive until the launch ran
         return du
 

@@ -153,6 +153,13 @@ def test_bench_self_launch_gloo():
     rec = json.loads(line)
     assert rec["n_gpus"] == 2 and rec["backend"] == "gloo"
     assert sorted(r["rank"] for r in rec["ranks_seen"]) == [0, 1]
+    # the N > 1 collective fields: the early MLP + gate
+    # bucket and 4 grid buckets, timed, with the bytes each rank moves
+    c = rec["comm"]
+    assert c["mean_ok"] and c["buckets_per_step"] == 5 and c["allreduce_ms"] > 0
+    from radnerf_amd import layout as LY
+    n = (2 * int(LY.grid_levels(0.5)["n_entries"]) + 2 * LY.FIELD_PARAMS + LY.gate_params(2)) * 4
+    assert c["bytes_per_rank"] == n and c["ring_bytes_per_rank"] == n
 
 
 def test_bench_world_mismatch_fails():

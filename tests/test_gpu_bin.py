@@ -1,0 +1,168 @@
+"""Binned ("store and sum") grid-gradient scatter (fx_mode 4: the walk appends
+fixed-point records to pages, rn_grid_bin sorts each page by slice, rn_grid_sum
+adds each slice in LDS; csrc/rn_bin.h, scatter.hip).
+
+* the bin + sum passes alone, on synthetic pages: every entry equals the
+  exact integer sum of its records times 2^-e_l (bit-exact), in place and
+  out of place, with pages of mixed levels, partial pages and empty slices;
+* the renderer at scale 16 (where it is the default) and, forced, at scale
+  0.5: every level's gradient matches the fp32-atomic backward of the same
+  step within FX_LEVEL_TOL (the oracle bars are in test_gpu_ml.py, which runs
+  the default path), the MLP / gate gradients are unchanged, and the grid
+  gradient is bitwise identical from step to step (exact int64 sums);
+* a record past the int22 range (a scale forced 2^10 too large) and a pool
+  too small for the step both set the redo flag, and the step's result is the
+  fp32 one; the pool then grows, and the next steps are binned again.
+"""
+import numpy as np
+import pytest
+import torch
+
+from radnerf_amd import layout as LY
+from radnerf_amd._lib import lib
+from radnerf_amd.fused import get_renderer, ml_render_fused
+from test_gpu_ml import FX_LEVEL_TOL, _run, _setup, check_fx_vs_fp32
+
+pytestmark = pytest.mark.gpu
+
+
+def _pack(idx, q0, q1, lay):
+    ib, vb = lay["idx_bits"], lay["v_bits"]
+    m = (1 << vb) - 1
+    return (idx.astype(np.uint64) | ((q0.astype(np.int64) & m).astype(np.uint64) << np.uint64(ib))
+            | ((q1.astype(np.int64) & m).astype(np.uint64) << np.uint64(ib + vb))).view(np.int64)
+
+
+@pytest.mark.parametrize("in_place", [True, False])
+def test_bin_sum_exact_on_synthetic_pages(cuda, in_place):
+    L = lib()
+    lay = L.bin_layout()
+    PAGE = lay["page"]
+    scale = 16.0
+    lv = LY.grid_levels(scale)
+    rng = np.random.default_rng(7)
+    vmax = (1 << (lay["v_bits"] - 1)) - 1
+    pages, metas, per = [], [], []
+    for l in range(16):
+        hs = int(lv["hsize"][l])
+        n = int(rng.integers(0, 3 * PAGE)) if l != 5 else 0          # level 5: no records
+        idx = rng.integers(0, hs, n)
+        if l == 15:                         # one hot entry and the range ends
+            idx[: n // 4] = hs - 1
+            idx[n // 4: n // 4 + 10] = 0
+        q0 = rng.integers(-vmax, vmax + 1, n)
+        q1 = rng.integers(-vmax, vmax + 1, n)
+        per.append((idx, q0, q1))
+        rec = _pack(idx, q0, q1, lay)
+        fill = int(rng.integers(PAGE // 2, PAGE + 1))                # partial pages
+        for a in range(0, n, fill):
+            c = rec[a:a + fill]
+            pg = np.zeros(PAGE, np.int64)
+            pg[:len(c)] = c
+            pages.append(pg)
+            metas.append(l | (len(c) << 8))
+    order = rng.permutation(len(pages))
+    pool = len(pages) + 3
+    i32 = dict(device=cuda, dtype=torch.int32)
+    ctl = torch.zeros(lay["ctl_bytes"] // 4, **i32)
+    ctl[0] = len(pages)
+    meta = torch.zeros(pool, **i32)
+    meta[:len(pages)] = torch.from_numpy(np.array([metas[i] for i in order], np.int32))
+    pin = torch.zeros(pool * PAGE, device=cuda, dtype=torch.int64)
+    pin[:len(pages) * PAGE] = torch.from_numpy(np.stack([pages[i] for i in order]).ravel())
+    pout = pin if in_place else torch.zeros_like(pin)
+    desc = torch.zeros(pool * lay["bins"], **i32)
+    lpages = torch.zeros(16 * pool, **i32)
+    sc = (2.0 ** rng.integers(-3, 12, 16)).astype(np.float32)
+    sc_t = torch.from_numpy(sc).to(cuda)
+    grad0 = rng.standard_normal(int(lv["n_entries"]) * 2).astype(np.float32)
+    grad = torch.from_numpy(grad0).to(cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    L.grid_bin(ctl.data_ptr(), meta.data_ptr(), pin.data_ptr(), pout.data_ptr(), desc.data_ptr(),
+               lpages.data_ptr(), pool, 64, st)
+    L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, ctl.data_ptr(),
+               desc.data_ptr(), lpages.data_ptr(), pout.data_ptr(), pool, sc_t.data_ptr(), None,
+               grad.data_ptr(), st)
+    got = grad.cpu().numpy().reshape(-1, 2)
+    want = grad0.copy().reshape(-1, 2)
+    for l, (idx, q0, q1) in enumerate(per):
+        off, hs = int(lv["offset"][l]), int(lv["hsize"][l])
+        a0 = np.zeros(hs, np.int64)
+        a1 = np.zeros(hs, np.int64)
+        np.add.at(a0, idx, q0)
+        np.add.at(a1, idx, q1)
+        inv = np.float32(1.0) / sc[l]
+        nz = (a0 != 0) | (a1 != 0)
+        blk = want[off:off + hs]
+        blk[nz, 0] = blk[nz, 0] + a0[nz].astype(np.float32) * inv
+        blk[nz, 1] = blk[nz, 1] + a1[nz].astype(np.float32) * inv
+    assert np.array_equal(got, want)
+    # each level's page list holds its pages
+    npg = ctl[1:17].cpu().numpy()
+    assert npg.tolist() == [sum(1 for m_ in metas if (m_ & 31) == l) for l in range(16)]
+
+
+def _levels(g, lv):
+    return [g.view(-1, 2)[int(lv["offset"][l]):int(lv["offset"][l]) + int(lv["hsize"][l])]
+            for l in range(16)]
+
+
+@pytest.mark.parametrize("B,K,scale", [(1024, 4, 16.0), (2048, 2, 0.5)])
+def test_binned_matches_fp32_and_is_reproducible(cuda, B, K, scale):
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    assert r.grid_fx
+    assert r.grid_bin == (scale > 0.5)
+    r.grid_bin = True
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)      # fp32: scales
+    _, gb1 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    assert check_fx_vs_fp32(m, gb1, g32, r, f"binned B{B} K{K} s{scale}") == 16
+    pool = r.ws._bin
+    assert int(pool["ctl"][0]) > 0                       # the walk took pages
+    assert int(pool["ctl"][0]) <= pool["pages"]
+    _, gb2 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    lv = LY.grid_levels(scale)
+    for l, (a, b) in enumerate(zip(_levels(gb1[0], lv), _levels(gb2[0], lv))):
+        assert torch.equal(a, b), l                      # exact integer sums
+    assert int(r.ws._fx[0].abs().max()) == 0             # the int32 table is unused
+
+
+def test_binned_record_overflow_redo(cuda):
+    B, K, scale = 1024, 4, 16.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    assert r.grid_bin
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    acc, scales, stats, redo = r.ws._fx
+    with torch.no_grad():
+        cur = scales[r.ws.fx_i]
+        cur.mul_(2.0 ** 10)          # the largest records map to ~2^28 units: past int22
+    _, g_redo = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    assert int(redo[0]) == 1
+    for x, y in zip(g_redo, g32):
+        assert float((x - y).norm() / y.norm().clamp_min(1e-30)) <= 1e-5     # fp32 order only
+    _, gb = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    assert int(redo[0]) == 0
+    check_fx_vs_fp32(m, gb, g32, r, "binned after redo")
+
+
+def test_binned_pool_overflow_redo_then_grows(cuda):
+    B, K, scale = 1024, 4, 16.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    r.bin_records_per_pair = 8           # a pool far too small for the step
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    _, g_redo = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    pool = r.ws._bin
+    redo = r.ws._fx[3]
+    assert int(pool["ctl"][0]) > pool["pages"]           # the walk ran out of pages
+    assert int(redo[0]) == 1
+    for x, y in zip(g_redo, g32):
+        assert float((x - y).norm() / y.norm().clamp_min(1e-30)) <= 1e-5
+    torch.cuda.synchronize()
+    _, gb = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)   # grown
+    assert r.ws._bin["pages"] > pool["pages"]
+    assert int(redo[0]) == 0
+    check_fx_vs_fp32(m, gb, g32, r, "binned after pool growth")
+    assert FX_LEVEL_TOL > 0

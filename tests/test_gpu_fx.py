@@ -193,3 +193,49 @@ def test_fx_per_entry_agreement(cuda, capsys):
     assert f_agree >= 0.999
     assert f_lost <= 0.05
     assert rel <= 0.04
+
+
+def _fx_weight(i):
+    return (int(i) * 2654435761) & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("wrapped", [True, False])
+def test_fx_opposite_wraps_set_redo(cuda, wrapped):
+    """ADVICE r03 / VERDICT r03 item 5: two int32 entries of one level that wrap
+    in opposite directions in one step (+2^32 and -2^32) leave the level's
+    plain entry sum equal to its record sum; the position-weighted sums
+    (element i weighted by (i * 2654435761) mod 2^32, mod 2^64) still differ,
+    so rn_grid_fx_fold sets the redo flag.  Control: the same records without
+    a wrap pass."""
+    from radnerf_amd._lib import lib
+    L = lib()
+    scale = 0.5
+    lv = LY.grid_levels(scale)
+    n_el = 2 * int(lv["n_entries"])
+    l = 15
+    a = 2 * int(lv["offset"][l]) + 10
+    b = 2 * int(lv["offset"][l]) + 1001
+    rec_a, rec_b = (2 ** 31 + 100, -(2 ** 31 + 100)) if wrapped else (100, -100)
+    ent_a = rec_a - 2 ** 32 if wrapped else rec_a          # the int32 entries as stored
+    ent_b = rec_b + 2 ** 32 if wrapped else rec_b
+    acc = torch.zeros(n_el, dtype=torch.int32, device=cuda)
+    acc[a], acc[b] = ent_a, ent_b
+    stats = np.zeros(160, np.int32)
+    st64 = stats.view(np.int64)                             # qsum @16, esum @32, wq @48, we @64 (i64 slots)
+    stats.view(np.uint32)[l] = np.float32(1.0).view(np.uint32)   # vmax: a small record
+    st64[16 + l] = rec_a + rec_b                            # qsum: exact record sum (0)
+    wq = (rec_a * _fx_weight(a) + rec_b * _fx_weight(b)) % (1 << 64)
+    st64[48 + l] = wq if wq < (1 << 63) else wq - (1 << 64)
+    stats_t = torch.from_numpy(stats).to(cuda)
+    scales = torch.full((2, 16), 2.0 ** 10, device=cuda)
+    redo = torch.zeros(1, dtype=torch.int32, device=cuda)
+    grad = torch.zeros(n_el, device=cuda)
+    assert ent_a + ent_b == rec_a + rec_b                  # the plain sums agree either way
+    L.grid_fx_fold(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, lv["res"].ctypes.data,
+                   acc.data_ptr(), scales[0].data_ptr(), scales[1].data_ptr(), stats_t.data_ptr(),
+                   redo.data_ptr(), grad.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert int(redo[0]) == (1 if wrapped else 0)
+    if not wrapped:                                         # folded: entry * 2^-10
+        assert float(grad[a]) == 100 / 1024 and float(grad[b]) == -100 / 1024
+    assert int(acc.abs().max()) == 0                        # re-zeroed either way

@@ -1,5 +1,6 @@
 """CPU: the merged-pass entry points (rn_bwd_plan, rn_field_fwd_merged,
-rn_field_bwd_merged, rn_grid_fx_fold, rn_seed_scale, rn_igrad_to_f32) reject bad arguments
+rn_field_bwd_merged, rn_grid_fx_fold, rn_grid_bin, rn_grid_sum, rn_grid_binned_fold,
+rn_seed_scale, rn_igrad_to_f32) reject bad arguments
 before any HIP call, with the messages include/radnerf.h documents."""
 import ctypes
 
@@ -24,18 +25,30 @@ def test_merged_entry_points_validate_without_gpu():
         L.field_fwd_merged(*[V] * 8, 8, 2, *[V] * 10, None, V, V, 256, 512, None)
     # scratch must hold a chunk plus one ray of every model
     with pytest.raises(RuntimeError, match="scratch_rows must be"):
-        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 2047, None, 1024, 256, *P[:7], 0, None)
+        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 2047, None, 1024, 256, *P[:7], 0, *P[:3], 0, None)
     with pytest.raises(RuntimeError, match="integer mode needs"):
         L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256,
-                           ctypes.c_void_p(8), None, None, *P[:4], 0, None)
+                           ctypes.c_void_p(8), None, None, *P[:4], 0, *P[:3], 0, None)
     with pytest.raises(RuntimeError, match="fx_mode"):
-        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 1, None)
+        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 1, *P[:3], 0, None)
     with pytest.raises(RuntimeError, match="fixed-point mode needs"):
-        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 2, None)
+        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 2, *P[:3], 0, None)
     with pytest.raises(RuntimeError, match="redo needs"):
-        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 3, None)
+        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 3, *P[:3], 0, None)
+    with pytest.raises(RuntimeError, match="binned mode needs"):
+        L.field_bwd_merged(*P[:10], 8, 2, 1024, *P[:14], 4096, None, 1024, 256, *P[:7], 4,
+                           *P[:3], 0, None)
     with pytest.raises(RuntimeError, match="null pointer"):
         L.grid_fx_fold(*P[:10])
+    with pytest.raises(RuntimeError, match="null pointer"):
+        L.grid_bin(*P[:6], 16, 2048, None)
+    with pytest.raises(RuntimeError, match="bad sizes"):
+        L.grid_bin(*[V] * 6, 0, 2048, None)
+    with pytest.raises(RuntimeError, match="null pointer"):
+        L.grid_sum(*P[:6], 16, None, None, None, None)
+    with pytest.raises(RuntimeError, match="null pointer"):
+        L.grid_binned_fold(*P[:8], 16, *P[:6])
+    assert L.version() == _lib.ABI_VERSION
     assert L.igrad_to_f32(0, None, None, None, None, None) == 0
     with pytest.raises(RuntimeError, match="null pointer"):
         L.seed_scale(None, None, 2, None, None, None, None, None, None)
