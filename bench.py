@@ -109,6 +109,9 @@ def parse():
     ap.add_argument("--grid-fx", type=int, default=None,
                     help="fixed-point grid-gradient accumulation: 1 on, 0 fp32 atomics "
                          "(default: the renderer's choice)")
+    ap.add_argument("--grid-bin", type=int, default=None,
+                    help="binned (store + sum) grid-gradient scatter 1/0 (default: the "
+                         "renderer's choice by shape)")
     ap.add_argument("--level-fwd", type=int, default=None,
                     help="level-partitioned field forward (rn_field_fwd_levels): 1 on, 0 the "
                          "merged forward (default: the renderer's choice)")
@@ -263,6 +266,8 @@ def main():
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     if args.grid_fx is not None:
         r.grid_fx = bool(args.grid_fx)
+    if args.grid_bin is not None:
+        r.grid_bin = bool(args.grid_bin) and r.grid_fx
     if args.level_fwd is not None:
         r.level_fwd = bool(args.level_fwd)
     if args.max_chunk:

@@ -26,7 +26,7 @@ namespace {
 #define GB_PER_THREAD (GB_PAGE / GB_BIN_THREADS)
 
 __global__ void __launch_bounds__(GB_BIN_THREADS)
-k_grid_bin(GbPool P) {
+k_grid_bin(GbPool P, bool rotate) {
     __shared__ uint64_t sRec[GB_PAGE];
     __shared__ uint32_t sHist[GB_MAX_BINS];
     const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
@@ -53,11 +53,20 @@ k_grid_bin(GbPool P) {
             }
         }
         __syncthreads();
-        if (wid == 0) {                 // exclusive scan of the bins, GB_BPL per lane
+        if (wid == 0) {
+            // exclusive scan of the bins, GB_BPL per lane, in an order rotated
+            // by the page (bin (j + rot) mod 256 is laid out j-th): slice b's
+            // run sits at a different offset of every page, so the sum pass's
+            // reads of one slice (one run per page) spread over the memory
+            // channels instead of repeating one offset at a 64-KB stride
             constexpr int GB_BPL = GB_MAX_BINS / 64;
+            const uint32_t rot = rotate ? (p * 97u) & (GB_MAX_BINS - 1u) : 0u;
             uint32_t h[GB_BPL], tot = 0u;
 #pragma unroll
-            for (int k = 0; k < GB_BPL; ++k) { h[k] = sHist[GB_BPL * lane + k]; tot += h[k]; }
+            for (int k = 0; k < GB_BPL; ++k) {
+                h[k] = sHist[(GB_BPL * lane + k + rot) & (GB_MAX_BINS - 1u)];
+                tot += h[k];
+            }
             uint32_t incl = tot;
 #pragma unroll
             for (int off = 1; off < 64; off <<= 1) {
@@ -68,8 +77,9 @@ k_grid_bin(GbPool P) {
             uint32_t* d = P.desc + (size_t)p * GB_MAX_BINS;
 #pragma unroll
             for (int k = 0; k < GB_BPL; ++k) {
-                d[GB_BPL * lane + k] = s0 | (h[k] << 16);
-                sHist[GB_BPL * lane + k] = s0;
+                const uint32_t bin = (GB_BPL * lane + k + rot) & (GB_MAX_BINS - 1u);
+                d[bin] = s0 | (h[k] << 16);
+                sHist[bin] = s0;
                 s0 += h[k];
             }
             if (lane == 0 && n > 0) {
@@ -211,7 +221,9 @@ int rn_grid_bin(void* ctl, const uint32_t* page_meta, const uint64_t* pages_in,
     P.ctl = (GbCtl*)ctl; P.page_meta = (uint32_t*)page_meta; P.pages_in = (uint64_t*)pages_in;
     P.pages_out = pages_out; P.desc = desc; P.level_pages = level_pages;
     P.pool_pages = (uint32_t)pool_pages;
-    k_grid_bin<<<blocks, GB_BIN_THREADS, 0, (hipStream_t)stream>>>(P);
+    // (ablation bit 20, timing only: no per-page rotation of the run layout)
+    const bool rotate = !((rn_debug_flags_internal() >> 20) & 1);
+    k_grid_bin<<<blocks, GB_BIN_THREADS, 0, (hipStream_t)stream>>>(P, rotate);
     RN_CHECK_LAUNCH();
     return 0;
 }

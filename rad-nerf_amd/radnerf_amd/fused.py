@@ -30,6 +30,10 @@ def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
 
+# per (device, stream): forward scratch shared by every workspace (level_buffers)
+_LEVEL_SCRATCH = {}
+
+
 class Workspace:
     """Persistent device buffers for one (B, K) configuration."""
 
@@ -77,14 +81,21 @@ class Workspace:
             self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
         return cap, self._chunks
 
-    def level_buffers(self):
+    def level_buffers(self, stream=None):
         """rn_field_fwd_levels' per-level encoding planes (16 x f16x2 per
-        sample slot, 64 B) and merged-order unit coordinates (16 B)."""
-        if getattr(self, "_levels", None) is None:
-            rows = self.feat.shape[0]
-            self._levels = (torch.empty(16, rows, device=self.device, dtype=torch.int32),
-                            torch.empty(rows, 4, device=self.device, dtype=torch.float32))
-        return self._levels
+        sample slot, 64 B) and merged-order unit coordinates (16 B).  They are
+        scratch of one forward (written by the encode, read by the MLP
+        tiles), so the workspaces of a device share one pair per stream,
+        grown to the largest (80 B per slot in every workspace
+        was ~40 % of a workspace)."""
+        rows = self.feat.shape[0]
+        key = (str(self.device), int(stream) if stream is not None else 0)
+        cur = _LEVEL_SCRATCH.get(key)
+        if cur is None or cur[0].shape[1] < rows:
+            cur = (torch.empty(16, rows, device=self.device, dtype=torch.int32),
+                   torch.empty(rows, 4, device=self.device, dtype=torch.float32))
+            _LEVEL_SCRATCH[key] = cur
+        return cur
 
     def fx_buffers(self, n, device):
         """Fixed-point grid-gradient state (rn_grid_fx_fold): int32 sums (n,
@@ -392,7 +403,7 @@ class FusedMLRenderer:
                   m.xyz_encoder.params_f16().data_ptr(), lo, lh, lr, ls, m._h_min.ctypes.data,
                   m._h_ext.ctypes.data, m.packed_frags().data_ptr())
         if fwd and self.level_fwd and (self.merged_bwd or self.merged_fwd):
-            planes, prep = w.level_buffers()
+            planes, prep = w.level_buffers(st)
             self._ev("field_fwd", L.field_fwd_levels, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
@@ -478,6 +489,7 @@ class FusedMLRenderer:
                 self._ev("fx_fold", L.grid_fx_fold, lo, lh, lr, acc.data_ptr(), cur.data_ptr(),
                          nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(),
                          st)
+            if use_fx:
                 self._ev("fx_redo", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                          rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                          w.seg_count.data_ptr(), w.mstart.data_ptr(),
@@ -502,7 +514,10 @@ class FusedMLRenderer:
         lay = lib().bin_layout()
         b = getattr(w, "_bin", None)
         if b is None:
-            need = -(-self.bin_records_per_pair * w.B * w.K // lay["page"])
+            # every wave keeps one page per level open (2 per wave of each
+            # persistent block), so a step fills pages only partly at small sizes
+            need = (-(-self.bin_records_per_pair * w.B * w.K // lay["page"]) +
+                    2 * 8 * self.merged_blocks)
         else:
             need = b["pages"]
             ev = b["seen_ev"]
@@ -713,7 +728,12 @@ def grad_unsupported(x, anchors, what):
 
 
 _RENDERERS = collections.OrderedDict()
-MAX_RENDERERS = 4       # workspaces are ~0.3 GB per 1k rays x sub-NeRF: keep a few
+# a workspace holds 1024 sample slots per (ray, sub-NeRF) at ~124 B each (t, dt,
+# ray, sigma, rgb, ws, their gradients, staging, the 64-B encoding cache, the
+# merged order): ~0.13 GB per 1k rays x sub-NeRFs; the level-partitioned
+# forward's planes (80 B per slot) and the binned scatter's page pool are
+# shared per device and stream / sized to the records: keep a few workspaces
+MAX_RENDERERS = 4
 
 
 def get_renderer(model, gating_net, n_rays, grad=True):
@@ -734,8 +754,10 @@ def get_renderer(model, gating_net, n_rays, grad=True):
 
 
 def release_renderers():
-    """Drop every cached renderer and its device workspace."""
+    """Drop every cached renderer and its device workspace (and the shared
+    forward scratch)."""
     _RENDERERS.clear()
+    _LEVEL_SCRATCH.clear()
 
 
 def ml_render_fused(model, gating_net, rays_o, rays_d, imgs_d, warmup=False, **kwargs):

@@ -200,6 +200,36 @@ class _TrainResults(dict):
         self[key] = v
         return v
 
+    # the lazy keys are keys of the result for every dict access path, not
+    # only [] / in: get, iteration, keys / values / items, len,
+    # dict(res) and copies materialise them like [] does
+    def get(self, key, default=None):
+        return self[key] if key in self else default
+
+    def _all(self):
+        for k in self.LAZY:
+            if not dict.__contains__(self, k):
+                self[k]
+        return self
+
+    def keys(self):
+        return dict.keys(self._all())
+
+    def values(self):
+        return dict.values(self._all())
+
+    def items(self):
+        return dict.items(self._all())
+
+    def __iter__(self):
+        return dict.__iter__(self._all())
+
+    def __len__(self):
+        return dict.__len__(self) + sum(1 for k in self.LAZY if not dict.__contains__(self, k))
+
+    def copy(self):
+        return dict(self.items())
+
 
 def _train_fused(model, rays_o, rays_d, kw):
     """rendering.py:192-239 on the fused K = 1 chain (radnerf_amd.fused):

@@ -75,6 +75,12 @@ def test_ngp_render_train_vs_oracle(cuda, fused):
                             [t(d_rgb), t(d_op), t(d_depth[:, 0])])
     for k in ("rays_a", "ws", "deltas", "ts", "rm_samples", "vr_samples"):
         assert k in res
+    # every dict access path sees the lazy keys: get, iteration,
+    # keys / items, len, dict(res)
+    lazy = {"rays_a", "ws", "deltas", "ts", "rm_samples", "vr_samples"}
+    assert res.get("ws") is not None and res.get("no such key", 7) == 7
+    assert lazy <= set(res) and lazy <= set(res.keys()) and lazy <= {k for k, _ in res.items()}
+    assert len(res) == len(list(res)) and lazy <= set(dict(res))
     n = int(res["rm_samples"])
     ra = res["rays_a"].cpu().numpy()
     assert ra.shape == (B, 3) and int(ra[:, 2].sum()) == n

@@ -164,6 +164,47 @@ def main():
             t.append(ev[1].elapsed_time(ev[2]))
         abl[name] = round(float(np.median(t)), 4)
     L.set_debug_flags(0)
+    # the bin pass without the per-page rotation of the run layout
+    L.set_debug_flags(1 << 20)
+    t = []
+    for it in range(reps):
+        pool.ctl.zero_()
+        pool.ctl[0] = n_pages
+        L.grid_bin(pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
+                   pool.pout.data_ptr(), pool.desc.data_ptr(), pool.lpages.data_ptr(),
+                   pool.pool_pages, 2048, sp)
+        ev[1].record(st)
+        L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
+                   pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
+                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+        ev[2].record(st)
+        torch.cuda.synchronize()
+        t.append(ev[1].elapsed_time(ev[2]))
+    abl["sum_unrotated_runs"] = round(float(np.median(t)), 4)
+    L.set_debug_flags(0)
+    pool.ctl.zero_()
+    pool.ctl[0] = n_pages
+    L.grid_bin(pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
+               pool.pout.data_ptr(), pool.desc.data_ptr(), pool.lpages.data_ptr(),
+               pool.pool_pages, 2048, sp)
+    # footprint test: the same runs, but every level's page list pointing at
+    # 16 of its pages only (tiny footprint: TLB- and cache-resident)
+    lp = pool.lpages.view(16, -1)
+    npg = pool.ctl[1:17].clone()
+    for l in range(16):
+        n = int(npg[l])
+        if n > 16:
+            lp[l, :n] = lp[l, torch.arange(n, device=dev) % 16]
+    t = []
+    for it in range(reps):
+        ev[1].record(st)
+        L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
+                   pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
+                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+        ev[2].record(st)
+        torch.cuda.synchronize()
+        t.append(ev[1].elapsed_time(ev[2]))
+    abl["sum_16_pages_per_level"] = round(float(np.median(t)), 4)
     tb, ts = float(np.median(tb)), float(np.median(ts))
     out = {"shape": shape, "layout": layout, "frac": frac, "records": n_rec, "pages": n_pages, "rel_err": float(err),
            "bin_ms": round(tb, 4), "sum_ms": round(ts, 4), "bin_sum_ms": round(tb + ts, 4),
