@@ -73,9 +73,21 @@ def config_label(K, scale, rays):
     return "custom"
 
 
-def workload_key(K, scale, rays, occupancy):
-    """Key of a workload's PMC pass in profiles/traffic.json (tools/pmc_traffic.py)."""
-    return f"K{K}_s{float(scale):g}_B{rays}_p{float(occupancy):.2f}"
+def mfma_measured(key, path=os.path.join(ROOT, "profiles", "mfma.json")):
+    """MFMA busy fraction and achieved TFLOP/s per kernel from the committed
+    counter pass of this workload (tools/gpu/mfma_r04.sh), or None."""
+    try:
+        with open(path) as f:
+            return json.load(f).get("workloads", {}).get(key)
+    except (OSError, ValueError):
+        return None
+
+
+def workload_key(K, scale, rays, occupancy, binned=False):
+    """Key of a workload's PMC pass in profiles/traffic.json (tools/pmc_traffic.py);
+    "_bin" when the grid gradient went through the binned scatter (its own pass:
+    the walk's page stores replace the atomics)."""
+    return f"K{K}_s{float(scale):g}_B{rays}_p{float(occupancy):.2f}" + ("_bin" if binned else "")
 
 
 def parse():
@@ -557,8 +569,10 @@ def main():
     # PMC figures only for a workload that has its own pass (tools/pmc_traffic.py
     # --merge keys them by K, scale, rays and occupancy); per launch, scaled by
     # this run's sample count where it differs from the profiled run's
-    traffic, atom_req, pmc_samples, pmc_key = None, None, None, workload_key(K, scale, B,
-                                                                             args.occupancy)
+    binned = bool(getattr(r, "grid_bin", False) and r.grid_fx and not args.split_bwd)
+    traffic, atom_req, pmc_samples, pmc_key = None, None, None, workload_key(
+        K, scale, B, args.occupancy, binned)
+    tj = None
     if os.path.exists(args.traffic_json) and not args.split_bwd:
         try:
             with open(args.traffic_json) as f:
@@ -596,6 +610,27 @@ def main():
                               "achieved": round(rate, 2), "peak": round(peak, 2), "unit": "G req/s",
                               "u32_share": u32_share,
                               "frac": round(rate / peak, 3)}
+        if binned:
+            # the walk issues no grid atomics in binned mode: the pass shows
+            # what is left (the dense levels' first fp32 step aside, none)
+            roofline["atomic"]["note"] = "binned scatter: PMC TCC_EA0_ATOMIC of the walk"
+    if binned and not atom_req:
+        roofline["atomic"] = None
+    if binned:
+        # the binned scatter's own passes (fx_fold = rn_grid_binned_fold: bin +
+        # check + sum): 8 B per record stored by the walk, 16 B moved by the bin
+        # pass (read + write), 8 B read by the sum pass
+        pool = r.ws._bin
+        npg = min(int(pool["ctl"][0]), pool["pages"])
+        recs = int((pool["meta"][:npg] >> 8).sum()) if npg else 0
+        fold_ms = kms.get("fx_fold", float("nan"))
+        roofline["binned"] = {
+            "records_per_launch": recs, "records_per_sample": round(recs / max(1, samples_per_step_rank), 2),
+            "pages": npg, "fold_ms": round(fold_ms, 4),
+            "fold_bytes": 24 * recs, "fold_GBs": round(24 * recs / (fold_ms * 1e-3) / 1e9, 1),
+            "fold_frac": round(24 * recs / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "fold_traffic": (tj or {}).get("grid_fold_bytes_per_launch"),
+            "walk_store_bytes": 8 * recs}
 
     rgb_linf = None
     cpu_base = None
@@ -633,6 +668,8 @@ def main():
                           "occupancy": args.occupancy,
                           "config": label,
                           "field_fwd": "levels" if getattr(r, "level_fwd", False) else "merged",
+                          "grid_scatter": ("binned" if binned else "fixed-point atomics"
+                                           if r.grid_fx and not args.split_bwd else "fp32 atomics"),
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": (f"pinned{args.pinned_sim}-rank0-sim" if args.pinned_sim
@@ -649,7 +686,11 @@ def main():
                # fwd+bwd, unpadded) at `value`, against the dense f16 peak
                "mfma": {"achieved": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6, 2),
                         "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6 / MFMA_F16_PEAK_TFLOPS, 5)},
+                        "frac": round(value / world * MLP_FLOP_PER_SAMPLE / 1e6 / MFMA_F16_PEAK_TFLOPS, 5),
+                        # measured: SQ_VALU_MFMA_BUSY_CYCLES per kernel of this
+                        # workload's rocprofv3 pass (tools/mfma_reduce.py,
+                        # profiles/mfma.json), None when it has no pass
+                        "measured": mfma_measured(pmc_key)},
                "kernel_ms": {k: round(v, 4) for k, v in sorted(kms.items())}}
         print(json.dumps(out), flush=True)
     if world > 1:

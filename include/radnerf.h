@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 2   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 3   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -281,20 +281,26 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
  * issuing memory-side atomics.  ctl: the 128-B GbCtl block (pages taken,
  * pages per level), zero before pass 1; page_meta [pool_pages] u32 (level |
  * count << 8); pages_in / pages_out [pool_pages][8192] u64; desc
- * [pool_pages][128] u32; level_pages [16][pool_pages] u32.
- * rn_grid_bin sorts each page by slice (8192 entries of its level) in LDS
- * into pages_out and writes each slice's run (start | count << 16) to desc
- * and the page to its level's list.  rn_grid_sum (one workgroup per slice,
- * 64 KB of LDS) adds the slice's runs of every page of its level into int64
+ * [pool_pages][256] u32; level_pages [16][pool_pages] u32.
+ * rn_grid_bin sorts each page by slice of its level (level_hsize [16]: a
+ * slice is the smallest power of two >= 64 entries that cuts the level into
+ * <= 128 slices, 4096 at most) in LDS into pages_out and writes each slice's
+ * run (start | count << 16) to desc and the page to its level's list.
+ * rn_grid_sum (one workgroup per slice, 64 KB of LDS; the same level_hsize)
+ * adds the slice's runs of every page of its level into int64
  * accumulators (exact, order-free) and then grid_grad += acc * 2^-e_l
  * (fx_scale) for every touched entry; it returns at once when *redo != 0.
  * Replaces the hash-grid parameter gradient of the tcnn GridEncoding
  * backward behind models/networks.py:300-328.                              */
+/* timing studies (debug bit 21): k_grid_sum per-phase wave cycles, read and
+ * reset (synchronous): [0..3] phases, [4] waves, [5] run groups, [6] / [7]
+ * earliest start / latest end (s_memrealtime ticks, 100 MHz) */
+int rn_debug_gb_cycles(unsigned long long* out);
 int rn_grid_bin_layout(int32_t* out);   /* host: page records, bins per page, slice
                                           entries, ctl bytes, index bits, value bits */
-int rn_grid_bin(void* ctl, const uint32_t* page_meta, const uint64_t* pages_in,
-                uint64_t* pages_out, uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
-                int32_t blocks, void* stream);
+int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
+                const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
+                uint32_t* level_pages, int32_t pool_pages, int32_t blocks, void* stream);
 /* rn_grid_bin + the binned redo / scale check (a record at 2^21 units, a
  * non-finite one, or a pool overflow sets *fx_redo; next scales 2^(18 - e))
  * + rn_grid_sum, for a fx_mode 4 backward; the caller then launches the

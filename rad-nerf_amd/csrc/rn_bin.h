@@ -17,9 +17,21 @@
 #include <stdint.h>
 
 #define GB_PAGE 8192              // records per page (64 KB)
-#define GB_SLICE_BITS 12          // entries per slice = 4096 (64 KB of int64 pairs in LDS)
+#define GB_SLICE_BITS 12          // largest slice: 4096 entries (64 KB of int64 pairs in LDS)
 #define GB_SLICE (1u << GB_SLICE_BITS)
+#define GB_MIN_SLICE_BITS 6       // smallest slice: 64 entries
 #define GB_MAX_BINS 256           // slices per level (level sizes <= 2^20 entries)
+
+// A level's slice size: the smallest power of two >= 64 that cuts the level
+// into at most 128 slices (4096 at the 2^19-entry hashed levels).  The dense
+// coarse levels get small slices, so their records spread over ~64-128
+// workgroups of the sum pass instead of 1-23 (level 0 at scale 16 is one 4096
+// slice: one workgroup took all its 1M records and set the pass's end).
+__host__ __device__ __forceinline__ uint32_t gb_slice_bits(uint32_t hsize) {
+    uint32_t b = GB_MIN_SLICE_BITS;
+    while (b < GB_SLICE_BITS && (hsize + (1u << b) - 1u) >> b > 128u) ++b;
+    return b;
+}
 #define GB_IDX_BITS 20            // entry index within its level
 #define GB_V_BITS 22              // each feature's fixed-point value, two's complement
 #define GB_V_MAX ((1 << (GB_V_BITS - 1)) - 1)
@@ -68,4 +80,5 @@ struct GbPool {
     uint32_t* desc;
     uint32_t* level_pages;
     uint32_t pool_pages;
+    uint8_t slice_bits[16];       // gb_slice_bits of each level's size
 };

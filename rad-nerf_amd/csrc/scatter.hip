@@ -19,9 +19,15 @@
 #include "rn_field.h"
 #include "rn_bin.h"
 
+// timing studies only (ablation bit 21): per-phase wave cycles of k_grid_sum
+// summed over waves ([0] LDS zero + barrier, [1] first run fetch, [2] run
+// loop, [3] write-back), [4] waves, [5] groups, [6] earliest wave start and
+// [7] latest wave end (s_memrealtime, 100 MHz)
+__device__ unsigned long long g_gb_cyc[8];
+
 namespace {
 
-#define GB_BIN_THREADS 256
+#define GB_BIN_THREADS 1024
 #define GB_SUM_THREADS 1024
 #define GB_PER_THREAD (GB_PAGE / GB_BIN_THREADS)
 
@@ -48,7 +54,7 @@ k_grid_bin(GbPool P, bool rotate) {
         for (int j = 0; j < GB_PER_THREAD; ++j) {
             const uint32_t i = tid + GB_BIN_THREADS * j;
             if (i < n) {
-                const uint32_t b = gb_idx(r[j]) >> GB_SLICE_BITS;
+                const uint32_t b = gb_idx(r[j]) >> P.slice_bits[l];
                 key[j] = (b << 16) | atomicAdd(&sHist[b], 1u);
             }
         }
@@ -106,29 +112,36 @@ struct GbSumArgs {
 };
 
 // ABL (timing studies only, tools/bin_probe.py): 1 no LDS adds (records
-// XOR-folded into a register), 2 int32 LDS adds instead of int64
+// XOR-folded into a register)
 template <int ABL>
-__device__ __forceinline__ void gb_add(int64_t* acc, uint64_t r, uint64_t& fold) {
-    const uint32_t e = gb_idx(r) & (GB_SLICE - 1u);
+__device__ __forceinline__ void gb_add(int64_t* acc, uint64_t r, uint64_t& fold, uint32_t emask) {
+    const uint32_t e = gb_idx(r) & emask;
     if (ABL == 1) {
         fold ^= r;
-    } else if (ABL == 2) {
-        int32_t* a32 = reinterpret_cast<int32_t*>(acc);
-        __hip_atomic_fetch_add(a32 + 2 * e, (int32_t)gb_v0(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        __hip_atomic_fetch_add(a32 + 2 * e + 1, (int32_t)gb_v1(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     } else {
         __hip_atomic_fetch_add(acc + 2 * e, gb_v0(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         __hip_atomic_fetch_add(acc + 2 * e + 1, gb_v1(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
 }
 
-#define GB_RUNS 16                // runs of one wave in flight
+#define GB_RUNS 8                 // runs of one wave in flight (up to 2 loads each)
 
-template <int ABL, int RUNS = GB_RUNS, bool NT = true>
+// Record loads are issued with every lane active: lane i reads record
+// start + i of the run's page (clamped into the page) and drops it in
+// registers when it lies past the run (the exec-masked form measured the same:
+// profiles/r04/binprobe/binprobe_full_s.json, bis1 / bis2).  What made the
+// first versions of this pass slow (4.1-4.6 ms at C5's volume) was one
+// workgroup: level 0 at scale 16 was a single 4096-entry slice taking all
+// 1M of its records, with one dependent load per 64 records (binprobe_full_s
+// vs _t: the long-run loads 8 in flight, 1.95 ms; vs _u: per-level slice
+// sizes, gb_slice_bits, 0.94 ms).
+template <int ABL, bool PROF = false, int BIS = 0>
 __global__ void __launch_bounds__(GB_SUM_THREADS, 8)   // two workgroups per CU
 k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t* __restrict__ redo,
            float* __restrict__ grad) {
     extern __shared__ int64_t acc[];               // [GB_SLICE][2]
+    uint64_t tp = PROF ? __builtin_amdgcn_s_memtime() : 0, cyc[4] = {0, 0, 0, 0}, ngrp = 0;
+    const uint64_t rt0 = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     if (redo && __builtin_nontemporal_load(redo) != 0) return;   // the fp32 redo replaces the step
     int q = 0;
 #pragma unroll
@@ -139,16 +152,27 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     const float sc = scale[l];
     if (npg == 0u || sc == 0.f) return;            // no records (an fp32 level went in by atomics)
     const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
-    for (int i = tid; i < 2 * (int)GB_SLICE; i += GB_SUM_THREADS) acc[i] = 0;
+    const uint32_t sbits = P.slice_bits[l], emask = (1u << sbits) - 1u;
+    for (int i = tid; i < (2 << sbits); i += GB_SUM_THREADS) acc[i] = 0;
     __syncthreads();
+    auto stamp = [&](int ph) {
+        if (PROF) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[ph] += t - tp; tp = t; }
+    };
+    stamp(0);
     const uint32_t* lp = P.level_pages + (size_t)l * P.pool_pages;
     constexpr uint32_t NW = GB_SUM_THREADS / RN_WAVE;
     // lane i of a wave holds page base + i's run of this slice (page, start |
-    // count << 16); the next batch's runs are loaded while this one is summed
+    // count << 16); the next batch's runs are loaded while this one is summed.
+    // The slices of a level walk its page list from different starting points
+    // (slice b at b / nslices of the list).
+    const uint32_t nsl = s.first[q + 1] - s.first[q];
+    const uint32_t start = (uint32_t)(((uint64_t)b * npg) / nsl);
     auto runs_of = [&](uint32_t base, uint32_t& pg, uint32_t& d) {
-        const uint32_t i = base + lane;
+        uint32_t i = base + lane;
         pg = 0u; d = 0u;
         if (i < npg) {
+            i += start;
+            i = i >= npg ? i - npg : i;
             pg = lp[i];
             d = P.desc[(size_t)pg * GB_MAX_BINS + b];
         }
@@ -156,40 +180,59 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     uint32_t pg, d;
     uint64_t fold = 0ull;
     runs_of(wid * 64u, pg, d);
+    if (PROF) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); stamp(1); }
     for (uint32_t base = wid * 64u; base < npg; base += NW * 64u) {
         const uint32_t pgc = pg, dc = d;
         runs_of(base + NW * 64u, pg, d);
 #pragma unroll 1
-        for (int k0 = 0; k0 < 64; k0 += RUNS) {
-            uint64_t r[RUNS];
-            uint32_t cnt[RUNS];
+        for (int k0 = 0; k0 < 64; k0 += GB_RUNS) {
+            ngrp += PROF ? 1 : 0;
+            uint64_t r0[GB_RUNS], r1[GB_RUNS];
+            uint32_t cnt[GB_RUNS], st[GB_RUNS];
+            const uint64_t* pgp[GB_RUNS];
 #pragma unroll
-            for (int j = 0; j < RUNS; ++j) {
+            for (int j = 0; j < GB_RUNS; ++j) {
                 const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
                 const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
-                cnt[j] = dk >> 16;
-                const uint64_t* run = P.pages_out + (size_t)pk * GB_PAGE + (dk & 0xffffu);
-                r[j] = (uint32_t)lane < cnt[j] ? (NT ? __builtin_nontemporal_load(run + lane) : run[lane])
-                                               : 0ull;
+                // BIS (timing bisection only): 1 load every run, 2 and fold every
+                // lane, 3 every run 64 records
+                cnt[j] = BIS == 3 ? 64u : dk >> 16;
+                st[j] = dk & 0xffffu;
+                pgp[j] = P.pages_out + (size_t)pk * GB_PAGE;
+                r0[j] = 0ull; r1[j] = 0ull;
+                if (BIS == 1 || BIS == 2 || cnt[j] != 0u)      // uniform: full-lane loads
+                    r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
+                if (cnt[j] > 64u)
+                    r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
             }
 #pragma unroll
-            for (int j = 0; j < RUNS; ++j) {
-                if ((uint32_t)lane < cnt[j]) gb_add<ABL>(acc, r[j], fold);
-                if (cnt[j] > 64u) {                // the rest of a longer run (uniform branch)
-                    const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
-                    const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
-                    const uint64_t* run = P.pages_out + (size_t)pk * GB_PAGE + (dk & 0xffffu);
-                    for (uint32_t o = 64u + lane; o < cnt[j]; o += 64u)
-                        gb_add<ABL>(acc, __builtin_nontemporal_load(run + o), fold);
+            for (int j = 0; j < GB_RUNS; ++j) {
+                if (BIS == 2 || (uint32_t)lane < cnt[j]) gb_add<ABL>(acc, r0[j], fold, emask);
+                if ((uint32_t)lane + 64u < cnt[j]) gb_add<ABL>(acc, r1[j], fold, emask);
+                // the rest of a run over 128 records (the coarse levels' runs are
+                // long): 8 full-lane loads in flight per step
+                for (uint32_t o = 128u; o < cnt[j]; o += 8u * 64u) {
+                    uint64_t rr[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        rr[u] = 0ull;
+                        if (o + 64u * u < cnt[j])          // uniform
+                            rr[u] = __builtin_nontemporal_load(
+                                pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
+                    }
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (o + 64u * u + lane < cnt[j]) gb_add<ABL>(acc, rr[u], fold, emask);
                 }
             }
         }
     }
+    stamp(2);
     __syncthreads();
     if (ABL == 1 && fold == 0x0123456789abcdefull) acc[0] = 1;    // keeps the loads
     const float inv = 1.0f / sc;                   // exact: a power of two
-    const uint32_t e0 = b * GB_SLICE;
-    const uint32_t ne = min(GB_SLICE, s.hs[l] - e0);
+    const uint32_t e0 = b << sbits;
+    const uint32_t ne = min(1u << sbits, s.hs[l] - e0);
     float2* g = reinterpret_cast<float2*>(grad) + (size_t)s.off[l] + e0;
     for (uint32_t e = tid; e < ne; e += GB_SUM_THREADS) {
         const int64_t a0 = acc[2 * e], a1 = acc[2 * e + 1];
@@ -199,11 +242,32 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
         v.y += (float)a1 * inv;
         g[e] = v;
     }
+    if (PROF) {
+        stamp(3);
+        if (lane == 0) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) atomicAdd(g_gb_cyc + qq, (unsigned long long)cyc[qq]);
+            atomicAdd(g_gb_cyc + 4, 1ull);
+            atomicAdd(g_gb_cyc + 5, (unsigned long long)ngrp);
+            atomicMin(g_gb_cyc + 6, (unsigned long long)rt0);
+            atomicMax(g_gb_cyc + 7, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        }
+    }
 }
 
 }  // namespace
 
 extern "C" {
+
+int rn_debug_gb_cycles(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gb_cyc), sizeof(unsigned long long) * 8, 0,
+                            hipMemcpyDeviceToHost) != hipSuccess)
+        return 2;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, ~0ull, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_gb_cyc), z, sizeof(z), 0, hipMemcpyHostToDevice) != hipSuccess)
+        return 2;
+    return 0;
+}
 
 int rn_grid_bin_layout(int32_t* out) {
     RN_CHECK_ARG(out, "null pointer");
@@ -212,12 +276,18 @@ int rn_grid_bin_layout(int32_t* out) {
     return 0;
 }
 
-int rn_grid_bin(void* ctl, const uint32_t* page_meta, const uint64_t* pages_in,
-                uint64_t* pages_out, uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
-                int32_t blocks, void* stream) {
-    RN_CHECK_ARG(ctl && page_meta && pages_in && pages_out && desc && level_pages, "null pointer");
+int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
+                const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
+                uint32_t* level_pages, int32_t pool_pages, int32_t blocks, void* stream) {
+    RN_CHECK_ARG(level_hsize && ctl && page_meta && pages_in && pages_out && desc && level_pages,
+                 "null pointer");
     RN_CHECK_ARG(pool_pages >= 1 && blocks >= 1, "bad sizes");
     GbPool P{};
+    for (int l = 0; l < RN_L; ++l) {
+        RN_CHECK_ARG(level_hsize[l] >= 1 && level_hsize[l] <= (GB_MAX_BINS << GB_SLICE_BITS) &&
+                         level_hsize[l] <= (1u << GB_IDX_BITS), "level too large for binning");
+        P.slice_bits[l] = (uint8_t)gb_slice_bits(level_hsize[l]);
+    }
     P.ctl = (GbCtl*)ctl; P.page_meta = (uint32_t*)page_meta; P.pages_in = (uint64_t*)pages_in;
     P.pages_out = pages_out; P.desc = desc; P.level_pages = level_pages;
     P.pool_pages = (uint32_t)pool_pages;
@@ -239,32 +309,33 @@ int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const
     uint32_t total = 0;
     for (int q = 0; q < RN_L; ++q) {            // the finest (heaviest) levels first
         const int l = RN_L - 1 - q;
-        RN_CHECK_ARG(level_hsize[l] <= (GB_MAX_BINS << GB_SLICE_BITS) &&
+        RN_CHECK_ARG(level_hsize[l] >= 1 && level_hsize[l] <= (GB_MAX_BINS << GB_SLICE_BITS) &&
                          level_hsize[l] <= (1u << GB_IDX_BITS), "level too large for binning");
         s.first[q] = total;
-        total += (level_hsize[l] + GB_SLICE - 1) / GB_SLICE;
+        const uint32_t sb = gb_slice_bits(level_hsize[l]);
+        total += (level_hsize[l] + (1u << sb) - 1) >> sb;
     }
     s.first[RN_L] = total;
     for (int l = 0; l < RN_L; ++l) { s.off[l] = level_offset[l]; s.hs[l] = level_hsize[l]; }
     GbPool P{};
     P.ctl = (GbCtl*)ctl; P.desc = (uint32_t*)desc; P.level_pages = (uint32_t*)level_pages;
     P.pages_out = (uint64_t*)pages_out; P.pool_pages = (uint32_t)pool_pages;
+    for (int l = 0; l < RN_L; ++l) P.slice_bits[l] = (uint8_t)gb_slice_bits(level_hsize[l]);
     const size_t lds = (size_t)GB_SLICE * 2 * sizeof(int64_t);
-    // ablations (timing studies only): bits 16-17 ABL, bit 18 plain loads,
-    // bit 19 32 runs in flight per wave
+    // ablations (timing studies only): bit 16 no LDS adds, bit 21 per-phase cycles
     const int dbg = rn_debug_flags_internal() >> 16;
-    const int abl = dbg & 3;
     hipStream_t st = (hipStream_t)stream;
-#define GB_SUM_LAUNCH(A, R, N) \
-    k_grid_sum<A, R, N><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad)
-    if (dbg == 0) GB_SUM_LAUNCH(0, GB_RUNS, true);
-    else if (abl == 1 && (dbg & 4)) GB_SUM_LAUNCH(1, GB_RUNS, false);
-    else if (abl == 1 && (dbg & 8)) GB_SUM_LAUNCH(1, 32, true);
-    else if (abl == 1) GB_SUM_LAUNCH(1, GB_RUNS, true);
-    else if (abl == 2) GB_SUM_LAUNCH(2, GB_RUNS, true);
-    else if (dbg & 4) GB_SUM_LAUNCH(0, GB_RUNS, false);
-    else if (dbg & 8) GB_SUM_LAUNCH(0, 32, true);
-    else GB_SUM_LAUNCH(0, GB_RUNS, true);
+#define GB_SUM_LAUNCH(A, PR) \
+    k_grid_sum<A, PR><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad)
+    if (dbg & 32) GB_SUM_LAUNCH(0, true);
+    else if ((dbg & 1) && (dbg & 0x1c)) {        // bits 18-20 with 16: bisection (timing)
+        const int bis = (dbg >> 2) & 7;
+        if (bis == 1) k_grid_sum<1, false, 1><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+        else if (bis == 2) k_grid_sum<1, false, 2><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+        else k_grid_sum<1, false, 3><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+    }
+    else if (dbg & 1) GB_SUM_LAUNCH(1, false);
+    else GB_SUM_LAUNCH(0, false);
 #undef GB_SUM_LAUNCH
     RN_CHECK_LAUNCH();
     return 0;
@@ -277,7 +348,7 @@ int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsiz
                         int32_t* fx_redo, float* grid_grad, void* stream) {
     RN_CHECK_ARG(fx_scale_cur && fx_scale_next && fx_stats && fx_redo, "null pointer");
     RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
-    int st = rn_grid_bin(ctl, page_meta, pages_in, pages_out, desc, level_pages, pool_pages,
+    int st = rn_grid_bin(level_hsize, ctl, page_meta, pages_in, pages_out, desc, level_pages, pool_pages,
                          2048, stream);
     if (st) return st;
     st = rn_fx_check_binned(fx_scale_cur, fx_scale_next, fx_stats, fx_redo, ctl,

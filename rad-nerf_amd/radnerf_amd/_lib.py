@@ -60,7 +60,8 @@ SIGNATURES = {
                             P, I32, P, P, P, I32, P],
     "rn_grid_fx_fold": [P, P, P, P, P, P, P, P, P, P],
     "rn_grid_bin_layout": [P],
-    "rn_grid_bin": [P, P, P, P, P, P, I32, I32, P],
+    "rn_debug_gb_cycles": [P],
+    "rn_grid_bin": [P, P, P, P, P, P, P, I32, I32, P],
     "rn_grid_sum": [P, P, P, P, P, P, I32, P, P, P, P],
     "rn_grid_binned_fold": [P, P, P, P, P, P, P, P, I32, P, P, P, P, P, P],
     "rn_render_test": [P, P, P, I64, I32, P, I64, I32, F32, F32, I32, I32, P, P, P, P, P, P, P,
@@ -84,7 +85,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 _lib = None
 
 

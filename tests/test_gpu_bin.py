@@ -78,7 +78,7 @@ def test_bin_sum_exact_on_synthetic_pages(cuda, in_place):
     grad0 = rng.standard_normal(int(lv["n_entries"]) * 2).astype(np.float32)
     grad = torch.from_numpy(grad0).to(cuda)
     st = torch.cuda.current_stream().cuda_stream
-    L.grid_bin(ctl.data_ptr(), meta.data_ptr(), pin.data_ptr(), pout.data_ptr(), desc.data_ptr(),
+    L.grid_bin(lv["hsize"].ctypes.data, ctl.data_ptr(), meta.data_ptr(), pin.data_ptr(), pout.data_ptr(), desc.data_ptr(),
                lpages.data_ptr(), pool, 64, st)
     L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, ctl.data_ptr(),
                desc.data_ptr(), lpages.data_ptr(), pout.data_ptr(), pool, sc_t.data_ptr(), None,

@@ -41,9 +41,9 @@ def test_merged_entry_points_validate_without_gpu():
     with pytest.raises(RuntimeError, match="null pointer"):
         L.grid_fx_fold(*P[:10])
     with pytest.raises(RuntimeError, match="null pointer"):
-        L.grid_bin(*P[:6], 16, 2048, None)
+        L.grid_bin(*P[:7], 16, 2048, None)
     with pytest.raises(RuntimeError, match="bad sizes"):
-        L.grid_bin(*[V] * 6, 0, 2048, None)
+        L.grid_bin(*[V] * 7, 0, 2048, None)
     with pytest.raises(RuntimeError, match="null pointer"):
         L.grid_sum(*P[:6], 16, None, None, None, None)
     with pytest.raises(RuntimeError, match="null pointer"):

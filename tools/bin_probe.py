@@ -131,7 +131,7 @@ def main():
         pool.ctl.zero_()
         pool.ctl[0] = n_pages
         ev[0].record(st)
-        L.grid_bin(pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
+        L.grid_bin(lv["hsize"].ctypes.data, pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
                    pool.pout.data_ptr(), pool.desc.data_ptr(), pool.lpages.data_ptr(),
                    pool.pool_pages, 2048, sp)
         ev[1].record(st)
@@ -149,9 +149,9 @@ def main():
         ts.append(ev[1].elapsed_time(ev[2]))
     # ablations of the sum pass (timing only): no LDS adds; int32 LDS adds
     abl = {}
-    for name, flag in (("sum_no_lds_adds", 1 << 16), ("sum_i32_adds", 2 << 16),
-                       ("sum_plain_loads", 4 << 16), ("sum_runs32", 8 << 16),
-                       ("sum_no_adds_plain", 5 << 16), ("sum_no_adds_runs32", 9 << 16)):
+    for name, flag in (("sum_no_lds_adds", 1 << 16), ("bis1_load_every_run", (1 << 16) | (1 << 18)),
+                       ("bis2_fold_every_lane", (1 << 16) | (2 << 18)),
+                       ("bis3_runs_of_64", (1 << 16) | (3 << 18))):
         L.set_debug_flags(flag)
         t = []
         for it in range(reps):
@@ -164,13 +164,32 @@ def main():
             t.append(ev[1].elapsed_time(ev[2]))
         abl[name] = round(float(np.median(t)), 4)
     L.set_debug_flags(0)
+    # per-phase cycles of the sum pass (debug bit 21)
+    import ctypes
+    cy = (ctypes.c_ulonglong * 8)()
+    L.debug_gb_cycles(cy)                  # reset
+    L.set_debug_flags(1 << 21)
+    ev[1].record(st)
+    L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
+               pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
+               pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+    ev[2].record(st)
+    torch.cuda.synchronize()
+    L.set_debug_flags(0)
+    L.debug_gb_cycles(cy)
+    waves = max(1, cy[4])
+    abl["sum_prof"] = {"ms": round(ev[1].elapsed_time(ev[2]), 4), "waves": cy[4],
+                       "groups_per_wave": round(cy[5] / waves, 2),
+                       "cycles_per_wave": {n: round(cy[i] / waves) for i, n in
+                                           enumerate(("zero", "first_fetch", "runs", "writeback"))},
+                       "span_ms_inside": round((cy[7] - cy[6]) / 1e5, 4)}
     # the bin pass without the per-page rotation of the run layout
     L.set_debug_flags(1 << 20)
     t = []
     for it in range(reps):
         pool.ctl.zero_()
         pool.ctl[0] = n_pages
-        L.grid_bin(pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
+        L.grid_bin(lv["hsize"].ctypes.data, pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
                    pool.pout.data_ptr(), pool.desc.data_ptr(), pool.lpages.data_ptr(),
                    pool.pool_pages, 2048, sp)
         ev[1].record(st)
@@ -184,7 +203,7 @@ def main():
     L.set_debug_flags(0)
     pool.ctl.zero_()
     pool.ctl[0] = n_pages
-    L.grid_bin(pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
+    L.grid_bin(lv["hsize"].ctypes.data, pool.ctl.data_ptr(), pool.meta.data_ptr(), pool.pin.data_ptr(),
                pool.pout.data_ptr(), pool.desc.data_ptr(), pool.lpages.data_ptr(),
                pool.pool_pages, 2048, sp)
     # footprint test: the same runs, but every level's page list pointing at

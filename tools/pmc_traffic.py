@@ -29,7 +29,9 @@ from collections import defaultdict
 # (the level-partitioned forward: prep + encode + MLP tiles), summed.
 KERNELS = {"field_bwd": (("k_field_bwd_merged",), ("k_field_bwd",)),
            "field_fwd": (("k_enc_prep", "k_field_encode_levels", "k_field_mlp_planes"),
-                         ("k_field_fwd_merged",), ("k_field_fwd",))}
+                         ("k_field_fwd_merged",), ("k_field_fwd",)),
+           # the binned scatter's bin + sum passes (fx_fold of a binned step)
+           "grid_fold": (("k_grid_bin", "k_grid_sum"),)}
 
 
 def per_dispatch(d):
@@ -57,7 +59,8 @@ def per_dispatch(d):
 def workload_key(cfg):
     """bench.py's key of a workload (keep in sync with bench.py workload_key)."""
     return (f"K{cfg['model_zoo_size']}_s{float(cfg['scale']):g}_B{cfg['rays_per_gpu']}"
-            f"_p{float(cfg.get('occupancy', 0.5)):.2f}")
+            f"_p{float(cfg.get('occupancy', 0.5)):.2f}"
+            + ("_bin" if cfg.get("grid_scatter") == "binned" else ""))
 
 
 def main():
