@@ -27,34 +27,43 @@ __device__ unsigned long long g_gb_cyc[8];
 
 namespace {
 
-#define GB_BIN_THREADS 1024
 #define GB_SUM_THREADS 1024
-#define GB_PER_THREAD (GB_PAGE / GB_BIN_THREADS)
 
-__global__ void __launch_bounds__(GB_BIN_THREADS)
+// THREADS per page; PF: the next page's records are loaded (all 8192, the
+// fill is not known yet) while this one is sorted
+template <int THREADS, bool PF>
+__global__ void __launch_bounds__(THREADS, THREADS / 128)   // two workgroups per CU
 k_grid_bin(GbPool P, bool rotate) {
+    constexpr int PT = GB_PAGE / THREADS;
     __shared__ uint64_t sRec[GB_PAGE];
     __shared__ uint32_t sHist[GB_MAX_BINS];
     const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
     const uint32_t np = min(__builtin_nontemporal_load(&P.ctl->pool_next), P.pool_pages);
+    uint64_t r[PT];
+    auto load_page = [&](uint32_t pg, uint64_t* dst, uint32_t n) {
+        const uint64_t* src = P.pages_in + (size_t)pg * GB_PAGE;
+#pragma unroll
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t i = tid + THREADS * j;
+            dst[j] = i < n ? __builtin_nontemporal_load(src + i) : 0ull;
+        }
+    };
+    if (PF && blockIdx.x < np) load_page(blockIdx.x, r, GB_PAGE);
     for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
         const uint32_t meta = P.page_meta[p];
         const uint32_t l = meta & 31u, n = meta >> 8;
-        for (int i = tid; i < GB_MAX_BINS; i += GB_BIN_THREADS) sHist[i] = 0u;
+        for (int i = tid; i < GB_MAX_BINS; i += THREADS) sHist[i] = 0u;
         __syncthreads();
-        const uint64_t* src = P.pages_in + (size_t)p * GB_PAGE;
-        uint64_t r[GB_PER_THREAD];
-        uint32_t key[GB_PER_THREAD];
+        if (!PF) load_page(p, r, n);
+        uint64_t rn[PF ? PT : 1];
+        if (PF && p + gridDim.x < np) load_page(p + gridDim.x, rn, GB_PAGE);
+        uint32_t key[PT];
+        const uint32_t sb = P.slice_bits[l];
 #pragma unroll
-        for (int j = 0; j < GB_PER_THREAD; ++j) {
-            const uint32_t i = tid + GB_BIN_THREADS * j;
-            r[j] = i < n ? __builtin_nontemporal_load(src + i) : 0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < GB_PER_THREAD; ++j) {
-            const uint32_t i = tid + GB_BIN_THREADS * j;
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t i = tid + THREADS * j;
             if (i < n) {
-                const uint32_t b = gb_idx(r[j]) >> P.slice_bits[l];
+                const uint32_t b = gb_idx(r[j]) >> sb;
                 key[j] = (b << 16) | atomicAdd(&sHist[b], 1u);
             }
         }
@@ -95,14 +104,18 @@ k_grid_bin(GbPool P, bool rotate) {
         }
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < GB_PER_THREAD; ++j) {
-            const uint32_t i = tid + GB_BIN_THREADS * j;
+        for (int j = 0; j < PT; ++j) {
+            const uint32_t i = tid + THREADS * j;
             if (i < n) sRec[sHist[key[j] >> 16] + (key[j] & 0xffffu)] = r[j];
         }
         __syncthreads();
         uint64_t* dst = P.pages_out + (size_t)p * GB_PAGE;
 #pragma unroll 4
-        for (uint32_t i = tid; i < n; i += GB_BIN_THREADS) __builtin_nontemporal_store(sRec[i], dst + i);
+        for (uint32_t i = tid; i < n; i += THREADS) __builtin_nontemporal_store(sRec[i], dst + i);
+        if (PF) {
+#pragma unroll
+            for (int j = 0; j < PT; ++j) r[j] = rn[j];
+        }
     }
 }
 
@@ -125,11 +138,13 @@ __device__ __forceinline__ void gb_add(int64_t* acc, uint64_t r, uint64_t& fold,
 }
 
 #define GB_RUNS 8                 // runs of one wave in flight (up to 2 loads each)
+static_assert(GB_RUNS == 8, "k_grid_sum deals pages to the waves in groups of 8 lanes");
 
 // Record loads are issued with every lane active: lane i reads record
 // start + i of the run's page (clamped into the page) and drops it in
-// registers when it lies past the run (the exec-masked form measured the same:
-// profiles/r04/binprobe/binprobe_full_s.json, bis1 / bis2).  What made the
+// registers when it lies past the run (ablation BIS 4: exec-masked loads).
+// Loading empty runs too and folding every lane measured within 10 %
+// (profiles/r04/binprobe/binprobe_full_s.json, bis1 / bis2).  What made the
 // first versions of this pass slow (4.1-4.6 ms at C5's volume) was one
 // workgroup: level 0 at scale 16 was a single 4096-entry slice taking all
 // 1M of its records, with one dependent load per 64 records (binprobe_full_s
@@ -161,14 +176,17 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     stamp(0);
     const uint32_t* lp = P.level_pages + (size_t)l * P.pool_pages;
     constexpr uint32_t NW = GB_SUM_THREADS / RN_WAVE;
-    // lane i of a wave holds page base + i's run of this slice (page, start |
-    // count << 16); the next batch's runs are loaded while this one is summed.
-    // The slices of a level walk its page list from different starting points
-    // (slice b at b / nslices of the list).
+    // A batch is 64 pages per wave: lane i of wave w holds the run of this
+    // slice (page, start | count << 16) of list entry base + (i / 8) * NW * 8 +
+    // w * 8 + i % 8 (groups of 8 pages dealt round-robin to the waves, so a
+    // level's last, partial batch still spreads over all of them); the next
+    // batch's runs are loaded while this one is summed.  The slices of a level
+    // walk its page list from different starting points (slice b at
+    // b / nslices of the list).
     const uint32_t nsl = s.first[q + 1] - s.first[q];
     const uint32_t start = (uint32_t)(((uint64_t)b * npg) / nsl);
     auto runs_of = [&](uint32_t base, uint32_t& pg, uint32_t& d) {
-        uint32_t i = base + lane;
+        uint32_t i = base + (lane >> 3) * (NW * GB_RUNS) + wid * GB_RUNS + (lane & 7);
         pg = 0u; d = 0u;
         if (i < npg) {
             i += start;
@@ -179,9 +197,9 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     };
     uint32_t pg, d;
     uint64_t fold = 0ull;
-    runs_of(wid * 64u, pg, d);
+    runs_of(0u, pg, d);
     if (PROF) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); stamp(1); }
-    for (uint32_t base = wid * 64u; base < npg; base += NW * 64u) {
+    for (uint32_t base = 0u; base < npg; base += NW * 64u) {
         const uint32_t pgc = pg, dc = d;
         runs_of(base + NW * 64u, pg, d);
 #pragma unroll 1
@@ -200,10 +218,17 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
                 st[j] = dk & 0xffffu;
                 pgp[j] = P.pages_out + (size_t)pk * GB_PAGE;
                 r0[j] = 0ull; r1[j] = 0ull;
-                if (BIS == 1 || BIS == 2 || cnt[j] != 0u)      // uniform: full-lane loads
-                    r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
-                if (cnt[j] > 64u)
-                    r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
+                if (BIS == 4) {                                 // exec-masked loads (timing)
+                    if ((uint32_t)lane < cnt[j])
+                        r0[j] = __builtin_nontemporal_load(pgp[j] + st[j] + lane);
+                    if ((uint32_t)lane + 64u < cnt[j])
+                        r1[j] = __builtin_nontemporal_load(pgp[j] + st[j] + 64u + lane);
+                } else {
+                    if (BIS == 1 || BIS == 2 || cnt[j] != 0u)  // uniform: full-lane loads
+                        r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
+                    if (cnt[j] > 64u)
+                        r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
+                }
             }
 #pragma unroll
             for (int j = 0; j < GB_RUNS; ++j) {
@@ -216,7 +241,7 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         rr[u] = 0ull;
-                        if (o + 64u * u < cnt[j])          // uniform
+                        if (BIS == 4 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
                             rr[u] = __builtin_nontemporal_load(
                                 pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
                     }
@@ -291,9 +316,16 @@ int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_met
     P.ctl = (GbCtl*)ctl; P.page_meta = (uint32_t*)page_meta; P.pages_in = (uint64_t*)pages_in;
     P.pages_out = pages_out; P.desc = desc; P.level_pages = level_pages;
     P.pool_pages = (uint32_t)pool_pages;
-    // (ablation bit 20, timing only: no per-page rotation of the run layout)
-    const bool rotate = !((rn_debug_flags_internal() >> 20) & 1);
-    k_grid_bin<<<blocks, GB_BIN_THREADS, 0, (hipStream_t)stream>>>(P, rotate);
+    // (timing studies only: bit 20 no per-page rotation of the run layout;
+    // bits 22-23 the variant: 1 = 512 threads with the next page prefetched,
+    // 2 = 256 threads)
+    const int dbg = rn_debug_flags_internal();
+    const bool rotate = !((dbg >> 20) & 1);
+    const int var = (dbg >> 22) & 3;
+    hipStream_t st = (hipStream_t)stream;
+    if (var == 1) k_grid_bin<512, true><<<blocks, 512, 0, st>>>(P, rotate);
+    else if (var == 2) k_grid_bin<256, false><<<blocks, 256, 0, st>>>(P, rotate);
+    else k_grid_bin<1024, false><<<blocks, 1024, 0, st>>>(P, rotate);
     RN_CHECK_LAUNCH();
     return 0;
 }
@@ -332,7 +364,8 @@ int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const
         const int bis = (dbg >> 2) & 7;
         if (bis == 1) k_grid_sum<1, false, 1><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
         else if (bis == 2) k_grid_sum<1, false, 2><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
-        else k_grid_sum<1, false, 3><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+        else if (bis == 3) k_grid_sum<1, false, 3><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+        else k_grid_sum<0, false, 4><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
     }
     else if (dbg & 1) GB_SUM_LAUNCH(1, false);
     else GB_SUM_LAUNCH(0, false);

@@ -151,7 +151,8 @@ def main():
     abl = {}
     for name, flag in (("sum_no_lds_adds", 1 << 16), ("bis1_load_every_run", (1 << 16) | (1 << 18)),
                        ("bis2_fold_every_lane", (1 << 16) | (2 << 18)),
-                       ("bis3_runs_of_64", (1 << 16) | (3 << 18))):
+                       ("bis3_runs_of_64", (1 << 16) | (3 << 18)),
+                       ("bis4_exec_masked_loads", (1 << 16) | (4 << 18))):
         L.set_debug_flags(flag)
         t = []
         for it in range(reps):
@@ -200,6 +201,21 @@ def main():
         torch.cuda.synchronize()
         t.append(ev[1].elapsed_time(ev[2]))
     abl["sum_unrotated_runs"] = round(float(np.median(t)), 4)
+    # bin pass variants (timing only): 512 threads + next page prefetched; 256 threads
+    for name, flag in (("bin_512_prefetch", 1 << 22), ("bin_256", 2 << 22)):
+        L.set_debug_flags(flag)
+        t = []
+        for it in range(reps):
+            pool.ctl.zero_()
+            pool.ctl[0] = n_pages
+            ev[0].record(st)
+            L.grid_bin(lv["hsize"].ctypes.data, pool.ctl.data_ptr(), pool.meta.data_ptr(),
+                       pool.pin.data_ptr(), pool.pout.data_ptr(), pool.desc.data_ptr(),
+                       pool.lpages.data_ptr(), pool.pool_pages, 2048, sp)
+            ev[1].record(st)
+            torch.cuda.synchronize()
+            t.append(ev[0].elapsed_time(ev[1]))
+        abl[name] = round(float(np.median(t)), 4)
     L.set_debug_flags(0)
     pool.ctl.zero_()
     pool.ctl[0] = n_pages
