@@ -52,3 +52,29 @@ def test_merged_entry_points_validate_without_gpu():
     assert L.igrad_to_f32(0, None, None, None, None, None) == 0
     with pytest.raises(RuntimeError, match="null pointer"):
         L.seed_scale(None, None, 2, None, None, None, None, None, None)
+
+
+def test_abi_constants_match_the_header():
+    """the binding's ABI version and buffer sizes are the header's (ADVICE r03:
+    a caller allocating an older size must not pass silently)"""
+    import os
+    import re
+
+    from radnerf_amd import fused
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "radnerf.h")).read()
+    assert int(re.search(r"#define RN_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION
+    assert int(re.search(r"#define RN_FX_STATS_BYTES (\d+)", hdr).group(1)) == fused.FX_STATS_BYTES
+    lay = _lib.lib().bin_layout()
+    assert lay == dict(page=8192, bins=256, slice=4096, ctl_bytes=128, idx_bits=20, v_bits=22)
+
+
+def test_grid_bin_and_sum_reject_oversized_levels():
+    import numpy as np
+    L = _lib.lib()
+    V = ctypes.c_void_p(8)
+    hs = np.full(16, 1 << 21, np.uint32)          # past the 20-bit entry index
+    with pytest.raises(RuntimeError, match="level too large"):
+        L.grid_bin(hs.ctypes.data, *[V] * 6, 16, 2048, None)
+    off = np.zeros(16, np.uint32)
+    with pytest.raises(RuntimeError, match="level too large"):
+        L.grid_sum(off.ctypes.data, hs.ctypes.data, *[V] * 4, 16, V, None, V, None)
