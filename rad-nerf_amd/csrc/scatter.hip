@@ -140,13 +140,12 @@ __device__ __forceinline__ void gb_add(int64_t* acc, uint64_t r, uint64_t& fold,
 #define GB_RUNS 8                 // runs of one wave in flight (up to 2 loads each)
 static_assert(GB_RUNS == 8, "k_grid_sum deals pages to the waves in groups of 8 lanes");
 
-// Record loads are issued with every lane active: lane i reads record
-// start + i of the run's page (clamped into the page) and drops it in
-// registers when it lies past the run (ablation BIS 4: exec-masked loads).
-// Loading empty runs too and folding every lane measured within 10 %
-// (profiles/r04/binprobe/binprobe_full_s.json, bis1 / bis2).  What made the
-// first versions of this pass slow (4.1-4.6 ms at C5's volume) was one
-// workgroup: level 0 at scale 16 was a single 4096-entry slice taking all
+// Record loads are issued by the run's lanes only (exec-masked): the pass
+// fetches the lines a run covers and nothing past it.  Full-lane loads
+// (clamped into the page, the tail dropped in registers) took 0.92 against
+// 0.70 ms at C5's volume (profiles/r04/binprobe/binprobe_full_v.json,
+// bis4).  What made the first versions of this pass slow (4.1-4.6 ms) was
+// one workgroup: level 0 at scale 16 was a single 4096-entry slice taking all
 // 1M of its records, with one dependent load per 64 records (binprobe_full_s
 // vs _t: the long-run loads 8 in flight, 1.95 ms; vs _u: per-level slice
 // sizes, gb_slice_bits, 0.94 ms).
@@ -212,19 +211,20 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
             for (int j = 0; j < GB_RUNS; ++j) {
                 const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
                 const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
-                // BIS (timing bisection only): 1 load every run, 2 and fold every
-                // lane, 3 every run 64 records
+                // BIS (timing bisection only, full-lane loads): 1 load every run,
+                // 2 and fold every lane, 3 every run 64 records, 4 as built
+                // before round 4's exec-masked loads
                 cnt[j] = BIS == 3 ? 64u : dk >> 16;
                 st[j] = dk & 0xffffu;
                 pgp[j] = P.pages_out + (size_t)pk * GB_PAGE;
                 r0[j] = 0ull; r1[j] = 0ull;
-                if (BIS == 4) {                                 // exec-masked loads (timing)
+                if (BIS == 0) {                                 // the run's lanes only
                     if ((uint32_t)lane < cnt[j])
                         r0[j] = __builtin_nontemporal_load(pgp[j] + st[j] + lane);
                     if ((uint32_t)lane + 64u < cnt[j])
                         r1[j] = __builtin_nontemporal_load(pgp[j] + st[j] + 64u + lane);
-                } else {
-                    if (BIS == 1 || BIS == 2 || cnt[j] != 0u)  // uniform: full-lane loads
+                } else {                                        // full-lane loads (timing)
+                    if (BIS != 4 || cnt[j] != 0u)
                         r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
                     if (cnt[j] > 64u)
                         r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
@@ -241,7 +241,7 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
 #pragma unroll
                     for (int u = 0; u < 8; ++u) {
                         rr[u] = 0ull;
-                        if (BIS == 4 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
+                        if (BIS == 0 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
                             rr[u] = __builtin_nontemporal_load(
                                 pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
                     }

@@ -152,7 +152,7 @@ def main():
     for name, flag in (("sum_no_lds_adds", 1 << 16), ("bis1_load_every_run", (1 << 16) | (1 << 18)),
                        ("bis2_fold_every_lane", (1 << 16) | (2 << 18)),
                        ("bis3_runs_of_64", (1 << 16) | (3 << 18)),
-                       ("bis4_exec_masked_loads", (1 << 16) | (4 << 18))):
+                       ("bis4_full_lane_loads", (1 << 16) | (4 << 18))):
         L.set_debug_flags(flag)
         t = []
         for it in range(reps):
