@@ -5,7 +5,8 @@ grid scatter at all, bit5 (32): rows staged but no walk (merged kernel).
 Token prefixes: none = merged backward (fixed-point hashed levels: the
 _field call includes rn_grid_fx_fold and the redo launch), "x" = merged
 backward with fp32 grid atomics, "s" = per-model backward, "i" = merged
-backward with integer accumulation, "f" = field_fwd.
+backward with integer accumulation, "a" = merged backward with the int32
+atomic scatter where the binned one is the default (scale 16), "f" = field_fwd.
 Workload from ABL_K / ABL_SCALE / ABL_RAYS (default C3)."""
 import ctypes
 import json
@@ -41,12 +42,20 @@ def main():
     nz = torch.from_numpy(S.noise(K, B)).to(dev)
     sd = [torch.from_numpy(a).to(dev) for a in S.loss_seeds(B, K)]
     bg = torch.ones(3, device=dev) if esf == 0 else torch.zeros(3, device=dev)
-    r = FusedMLRenderer(m, g, B)
-    _, _, _, gt, _ = r.forward(o, d, d, nz, bg, 1e-4, esf)
     gg = torch.zeros_like(m.xyz_encoder.params)
     mg = torch.zeros_like(m.mlp_params)
     ag = torch.zeros_like(g.params)
-    r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
+    rens = {}
+    for key in ("", "a"):          # "a": the int32 atomic scatter (own workspace and scales)
+        rr = FusedMLRenderer(m, g, B)
+        if key == "a":
+            rr.grid_bin = False
+        for _ in range(2):         # the first backward is fp32 and sets the scales
+            _, _, _, gt, _ = rr.forward(o, d, d, nz, bg, 1e-4, esf)
+            rr.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
+        rr.trace = {"field_bwd", "fx_fold"}
+        rens[key] = rr
+    kern = {}
     L = lib()
     st = torch.cuda.current_stream().cuda_stream
     # tokens: "<flags>" = field_bwd (merged) with debug flags, "s<flags>" = the
@@ -56,7 +65,18 @@ def main():
     fwd = []
     for rnd in range(5):
         for f in flags:
-            L.set_debug_flags(int(f.lstrip("fsix")))
+            L.set_debug_flags(int(f.lstrip("fsixa")))
+            r = rens["a" if f.startswith("a") else ""]
+            r.events = {}
+            # the fixed-point scales as the primed steps left them: a timing
+            # flag (no records, no vmax) must not steer the next token's scales
+            fx = getattr(r.ws, "_fx", None)
+            if fx is not None:
+                if not hasattr(r, "_abl_fx"):
+                    r._abl_fx = (fx[1].clone(), r.ws.fx_i)
+                fx[1].copy_(r._abl_fx[0])
+                r.ws.fx_i = r._abl_fx[1]
+                fx[3].zero_()
             r.merged_bwd = not f.startswith("s")
             r.int_grad = f.startswith("i")
             r.grid_fx = not f.startswith("x")      # "x": fp32 grid atomics
@@ -69,11 +89,14 @@ def main():
             b.record()
             torch.cuda.synchronize()
             times[f].append(a.elapsed_time(b))
-            if int(f.lstrip("fsix")) & 4096:
+            for kname, v in r.kernel_times_ms().items():
+                kern.setdefault(f, {}).setdefault(kname, []).extend(v)
+            if int(f.lstrip("fsixa")) & 4096:
                 cyc = (ctypes.c_ulonglong * 8)()
                 L.debug_cycles(ctypes.cast(cyc, ctypes.c_void_p).value)
                 phases.setdefault(f, []).append([int(c) for c in cyc[:4]])
         L.set_debug_flags(0)
+        r = rens[""]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
         r._field(True, o, d, st)
@@ -85,6 +108,10 @@ def main():
                             if not f.startswith("f")},
            "field_fwd_flags_ms": {str(f): float(np.median(v)) for f, v in times.items()
                                   if f.startswith("f")},
+           # the launches alone (HIP events on the launch stream): the merged
+           # backward and, fixed point, its fold (bin + check + sum when binned)
+           "kernel_ms": {f: {k: round(float(np.median(v)), 4) for k, v in kv.items()}
+                         for f, kv in kern.items()},
            # flag 4096: summed wave cycles per phase (MLP, staging, walk, chunk
            # tails), median over rounds, as fractions of their sum
            "phases": {f: dict(zip(("mlp", "staging", "walk", "tail"),

@@ -1,0 +1,7 @@
+#!/bin/bash
+# C5 merged-backward phases, binned scatter: with and without the page stores
+set -u
+mkdir -p gpurun_out
+TAG=${1:-y}
+export TMPDIR=/tmp
+ABL_K=8 ABL_SCALE=16 ABL_RAYS=8192 timeout -k 10 300 python3 tools/ablate.py 0 1 a0 a1 4 4096 4097 a4096 a4097 > gpurun_out/ablate_c5bin_$TAG.json 2> gpurun_out/ablate_c5bin_$TAG.err || exit $?
