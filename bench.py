@@ -295,9 +295,14 @@ def main():
     grid_rng, rest_rng = ar.param_range(0, 1), ar.param_range(1)
     comm_on = [world > 1]
     pending = []
+    # gloo's collectives on device tensors block the host until they complete:
+    # launched from inside the backward they stall the launch queue mid-step
+    # (the 2-rank gloo rehearsal on one GPU fell from 476 to 80 Msamples/s),
+    # so with gloo every bucket goes out after the backward
+    early_ok = world > 1 and dist.get_backend() == "nccl"
 
     def early_bucket():
-        if comm_on[0]:
+        if comm_on[0] and early_ok:
             main = torch.cuda.current_stream(dev)
             main.wait_stream(r._side(dev))       # the gate backward ran on the side stream
             pending.append(ar.launch_range(*rest_rng, 1))
@@ -361,8 +366,11 @@ def main():
             "ms_per_step_without": round(float(no_comm) / args.steps * 1e3, 4),
             "exposed_ms": round((float(with_comm) - float(no_comm)) / args.steps * 1e3, 4),
             "backend": dist.get_backend(),
-            "schedule": "MLP+gate bucket after field_bwd (beside the grid fold), grid in "
-                        f"{args.buckets} buckets after the backward; comm stream events"})
+            "schedule": ("MLP+gate bucket after field_bwd (beside the grid fold), grid in "
+                         f"{args.buckets} buckets after the backward; comm stream events"
+                         if early_ok else
+                         f"gloo: MLP+gate bucket and the grid in {args.buckets} buckets after the "
+                         "backward (host-blocking collectives); comm stream events")})
     # per-kernel breakdown: the same steps again with every launch traced
     # (after the timed region; not part of `value`)
     r.trace = True
