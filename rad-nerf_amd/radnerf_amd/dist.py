@@ -175,7 +175,8 @@ class GradAllReduce:
     def comm_stats(self, steps):
         """Per-step collective figures of the handles finished since
         reset_timing(): allreduce_ms (sum of the buckets' durations on the
-        comm stream), buckets per step, bytes per rank (payload and a ring
+        comm stream; host-timed backends: first launch to last completion of
+        each launch_range), buckets per step, bytes per rank (payload and a ring
         all-reduce's 2 (P-1)/P of it).  Synchronises."""
         world = dist.get_world_size() if dist.is_initialized() else 1
         tot, n_parts, payload = 0.0, 0, 0
@@ -184,10 +185,12 @@ class GradAllReduce:
                 if h["cuda"]:
                     a.synchronize(); b.synchronize()
                     tot += a.elapsed_time(b)
-                else:
-                    tot += (b - a) * 1e3
                 n_parts += 1
                 payload += (hi - lo) * self.flat.element_size()
+            if not h["cuda"] and h["parts"]:
+                # host-timed buckets are all in flight together: the span from
+                # the first launch to the last completion
+                tot += (max(b for _, _, b in h["parts"]) - min(a for _, a, _ in h["parts"])) * 1e3
         steps = max(1, int(steps))
         return {"allreduce_ms": round(tot / steps, 4), "buckets_per_step": n_parts / steps,
                 "bytes_per_rank": int(payload / steps),
