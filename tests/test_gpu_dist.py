@@ -71,6 +71,19 @@ def test_data_parallel_training_stays_identical(tmp_path):
     assert res["finite"]
 
 
+def test_data_parallel_training_stays_identical_binned(tmp_path):
+    """The same at scale 16, where the grid gradient goes through the binned
+    scatter (page stores, bin + exact int64 sums): the ranks' parameters,
+    grids and bitfields stay bit-identical over 14 Adam steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    res = _run_ranks("train_worker.py", tmp_path / "train16.json", timeout=110, extra=("16",))
+    print({k: v for k, v in res.items() if k != "losses"})
+    assert res["world"] == 2 and res["grid_bin"] and res["bin_pages"] > 0, res
+    assert all(res["identical"].values()), res["identical"]
+    assert res["finite"]
+
+
 def test_bucketed_adam_epilogue_matches_plain(tmp_path):
     """GradAllReduce.reduce_and_step (4 asynchronous all-reduce buckets, each
     bucket's division by the world size and FusedAdam update queued behind its

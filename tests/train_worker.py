@@ -2,8 +2,9 @@
 (not a test module): one rank of radnerf_amd.trainer.Trainer rehearsed with 2
 ranks on ONE GPU over gloo.  Each rank trains on its own rays for N steps
 (density-grid updates every 4 steps, warm-up updates over every cell first,
-Adam); at the end the ranks compare SHA-256 digests of their parameters,
-density grids and bitfields and rank 0 writes the result to argv[1]."""
+Adam; argv[2] the scale, 16: the binned grid scatter); at the end the ranks
+compare SHA-256 digests of their parameters, density grids and bitfields and
+rank 0 writes the result to argv[1]."""
 import hashlib
 import json
 import os
@@ -25,11 +26,11 @@ def digest(t):
     return hashlib.sha256(t.detach().cpu().contiguous().numpy().tobytes()).hexdigest()
 
 
-def main(out_path):
+def main(out_path, scale=0.5):
     rank, _, world = rdist.init(backend="gloo")
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
-    B, K, scale, n_steps = 1024, 2, 0.5, 14
+    B, K, n_steps = 1024, 2, 14
     model = MNGP(scale, size=K, seed=3)
     gate = Ray_Gate(K, seed=4)
     with torch.no_grad():
@@ -60,7 +61,10 @@ def main(out_path):
         occ = [float(getattr(model, f"density_bitfield_{i}").float().mean()) for i in range(K)]
         res = {"world": world, "identical": {k: all(a[k] == mine[k] for a in allr) for k in mine},
                "bitfields_changed": changed, "occupancy_byte_mean": occ, "losses": losses,
-               "finite": bool(all(torch.isfinite(v.float()).all() for v in state.values()))}
+               "finite": bool(all(torch.isfinite(v.float()).all() for v in state.values())),
+               "grid_bin": bool(tr.renderer.grid_bin and tr.renderer.grid_fx),
+               "bin_pages": (int(tr.renderer.ws._bin["ctl"][0])
+                             if getattr(tr.renderer.ws, "_bin", None) else 0)}
         with open(out_path, "w") as f:
             json.dump(res, f)
     dist.barrier()
@@ -68,4 +72,4 @@ def main(out_path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 0.5)
