@@ -13,6 +13,7 @@
 //    12 B sample record (t, dt, ray) instead of 32 B (xyz, dir, t, dt):
 //    xyz is recomputed bit-identically downstream as fmaf(t, d, o).
 #include "rn_march.h"
+#include "rn_bin.h"      // rn_debug_flags_internal
 #pragma clang fp contract(off)
 
 namespace {
@@ -273,7 +274,7 @@ inline MarchCfg make_cfg(int cascades, int grid_size, int max_samples, float sca
                          float dt_scale, float esf) {
     MarchCfg c;
     c.cascades = cascades; c.grid_size = grid_size; c.max_samples = max_samples;
-    c.scale = scale; c.dt_scale = dt_scale; c.esf = esf;
+    c.scale = scale; c.dt_scale = dt_scale; c.esf = esf; c.abl = 0;
     return c;
 }
 
@@ -491,6 +492,7 @@ int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* cen
     RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts,
                  "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
+    c.abl = (rn_debug_flags_internal() >> 24) & 1;
     if (stage_ts)
         k_ml_march_count<true><<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
             (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,

@@ -162,7 +162,7 @@ int rn_render_test(const float* rays_o, const float* rays_d, const float* hits_t
     g.hits = hits_t; g.bitfields = density_bitfields; g.bitfield_bytes = bitfield_bytes;
     // raymarching.cu:370,399: the test march hands `cascades` to calc_dt as its scale
     g.mc.cascades = cascades; g.mc.grid_size = grid_size; g.mc.max_samples = max_samples;
-    g.mc.scale = scale; g.mc.dt_scale = (float)cascades; g.mc.esf = exp_step_factor;
+    g.mc.scale = scale; g.mc.dt_scale = (float)cascades; g.mc.esf = exp_step_factor; g.mc.abl = 0;
     g.opacity = opacity; g.depth = depth; g.rgb = rgb; g.n_samples = n_samples;
     g.n_rays = (int)n_rays; g.max_samples = max_samples; g.thr = T_threshold;
     hipStream_t st = (hipStream_t)stream;

@@ -14,6 +14,7 @@ struct MarchCfg {
     float scale;      // used for mip_bound and (train) calc_dt
     float dt_scale;   // `scale` argument handed to calc_dt (== cascades for test)
     float esf;
+    int abl;          // timing studies only (debug bit 24): 1 = no t chain (wrong t)
 };
 
 struct NoSink {
@@ -171,6 +172,8 @@ __device__ int march_ray_wave(float ox, float oy, float oz, float dx, float dy, 
 #pragma unroll 16
                 for (int i = 0; i < RN_WAVE - 1; ++i) { const float nt = t + d0; t = i < lane ? nt : t; }
             }
+        } else if (c.abl & 1) {          // timing only: the chain's cost
+            t = fmaf((float)lane, rn_calc_dt(tb, c.esf, c.max_samples, c.grid_size, c.dt_scale), tb);
         } else {
 #pragma unroll 8
             for (int i = 0; i < RN_WAVE - 1; ++i) {
