@@ -464,9 +464,11 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                 ? ((q0 >> 12) & 0x3ffu) | (q1 << 10)
                 : (idx & ((1u << GB_IDX_BITS) - 1u)) | (q0 << 20);
             const uint32_t pg = odd ? W.pgB : W.pgA, n = odd ? W.nB : W.nA;
-            if (pg < G.pool_pages)
-                __builtin_nontemporal_store(
-                    word, reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane);
+            uint32_t* dst = reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane;
+            if (pg < G.pool_pages) {
+                if (dbg & 8) *dst = word;                // (timing only: plain stores)
+                else __builtin_nontemporal_store(word, dst);
+            }
         } else if (GM == 2 && fx_lvl) {
             const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
