@@ -2,17 +2,19 @@
 // field.hip GM 4, is pass 1: it appends each level's records to pages).
 //
 //   k_grid_bin  one workgroup per page: counting sort of the page's records
-//               by slice (GB_SLICE entries of the page's level) in LDS, the
-//               sorted page written back coalesced, plus each slice's run
-//               (start, count) and the page's entry in its level's page list;
+//               by slice of the page's level (gb_slice_bits: 64-4096 entries)
+//               in LDS, the sorted page written back coalesced, plus each
+//               slice's run (start, count) and the page's entry in its level's
+//               page list;
 //   k_grid_sum  one workgroup per slice: the slice's runs of every page of
 //               its level added into an int64 copy of the slice in LDS
 //               (ds_add_u64: exact and order-free), then
 //               grid_grad += acc * 2^-e_l once per touched entry.
 //
-// Both passes move 8 B per record with full-line accesses (pages of 64 KB,
-// runs of ~128 records at C5), against the 64-B memory-side request per
-// 1.84 records of the atomic form.  See rn_bin.h for the formats.
+// The bin pass reads and writes 8 B per record in whole pages, the sum pass
+// reads each run's lines (runs of ~64 records at the hashed levels, longer at
+// the dense ones), against the 64-B memory-side request per 1.84 records of
+// the atomic form.  See rn_bin.h for the formats.
 // Reference: the tcnn grid-encoding backward (hash-grid parameter gradient)
 // behind /root/reference/models/networks.py:300-328.
 #include "rn_common.h"
