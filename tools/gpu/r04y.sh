@@ -4,4 +4,4 @@ set -u
 mkdir -p gpurun_out
 TAG=${1:-y}
 export TMPDIR=/tmp
-ABL_K=8 ABL_SCALE=16 ABL_RAYS=8192 timeout -k 10 300 python3 tools/ablate.py 0 16 8 1 a0 a1 > gpurun_out/ablate_c5bin_$TAG.json 2> gpurun_out/ablate_c5bin_$TAG.err || exit $?
+ABL_K=8 ABL_SCALE=16 ABL_RAYS=8192 timeout -k 10 300 python3 tools/ablate.py 16 144 1 16 144 1 > gpurun_out/ablate_c5bin_$TAG.json 2> gpurun_out/ablate_c5bin_$TAG.err || exit $?
