@@ -108,7 +108,7 @@ class GradAllReduce:
         last = len(sizes) if last is None else last
         return sum(sizes[:first]), sum(sizes[:last])
 
-    def launch_range(self, a, b, n_buckets=1):
+    def launch_range(self, a, b, n_buckets=1, stream_ordered=None):
         """Start SUM all-reduces of flat[a:b] in n_buckets pieces as soon as the
         compute stream has produced them: on a comm stream that waits for the
         compute stream, bracketed by events there (CUDA), so the collectives
@@ -123,7 +123,11 @@ class GradAllReduce:
         # (nccl = RCCL); gloo blocks the host in wait(), so its buckets are all
         # launched first and timed on the host (waiting per bucket serialised
         # them: the 2-rank gloo rehearsal ran 305 instead of ~21 ms per step)
-        cuda = self.flat.is_cuda and dist.get_backend() == "nccl"
+        # (stream_ordered=True forces the comm-stream form on any backend: the
+        # GPU test runs it over gloo, the only multi-rank backend of a 1-GPU box)
+        if stream_ordered is None:
+            stream_ordered = dist.get_backend() == "nccl"
+        cuda = self.flat.is_cuda and bool(stream_ordered)
         handle = {"parts": [], "cuda": cuda}
         if cuda:
             main = torch.cuda.current_stream(self.flat.device)

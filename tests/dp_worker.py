@@ -56,6 +56,20 @@ def main(out_path):
     step(r, o, d, nz, sd, bg, ar.views)
     ar.reduce()
     torch.cuda.synchronize()
+    reduced = ar.flat.clone()
+    # the staged form bench.py uses over RCCL (comm stream, events, the MLP +
+    # gate bucket then the grid in 4 buckets), forced here over gloo: the same
+    # averaged buffer, and its timing fields
+    ar.zero()
+    ar.reset_timing()
+    step(r, o, d, nz, sd, bg, ar.views)
+    hs = [ar.launch_range(*ar.param_range(1), 1, stream_ordered=True),
+          ar.launch_range(*ar.param_range(0, 1), 4, stream_ordered=True)]
+    for h in hs:
+        ar.finish(h)
+    torch.cuda.synchronize()
+    staged_equal = bool(torch.equal(ar.flat, reduced))
+    stats = ar.comm_stats(1)
     if rank == 0:
         ref = rdist.GradAllReduce(params, dev)      # not reduced: a local buffer
         ref.zero()
@@ -65,7 +79,9 @@ def main(out_path):
         torch.cuda.synchronize()
         res = {"world": world, "grid_rel": rel(ar.views[0], ref.views[0]),
                "mlp_rel": rel(ar.views[1], ref.views[1]),
-               "gate_rel": rel(ar.views[2], ref.views[2])}
+               "gate_rel": rel(ar.views[2], ref.views[2]),
+               "staged_equal": staged_equal, "staged_stats": stats,
+               "staged_cuda": all(h["cuda"] for h in hs), "n_flat": ar.flat.numel()}
         with open(out_path, "w") as f:
             json.dump(res, f)
     dist.barrier()

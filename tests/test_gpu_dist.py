@@ -52,6 +52,11 @@ def test_data_parallel_two_ranks_one_gpu(tmp_path):
     res = _run_ranks("dp_worker.py", tmp_path / "dp.json")
     assert res["world"] == 2, res
     assert res["grid_rel"] <= 1e-4 and res["mlp_rel"] <= 1e-4 and res["gate_rel"] <= 1e-4, res
+    # the comm-stream staged all-reduce (bench.py's N > 1 form over RCCL), forced over gloo
+    assert res["staged_cuda"] and res["staged_equal"], res
+    st = res["staged_stats"]
+    assert st["buckets_per_step"] == 5 and st["allreduce_ms"] > 0, st
+    assert st["bytes_per_rank"] == 4 * res["n_flat"], st
 
 
 def test_data_parallel_training_stays_identical(tmp_path):
