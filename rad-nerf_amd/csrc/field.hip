@@ -1922,9 +1922,14 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
 #define PLANM_WAVES 2
 #define PLANM_LDS 2048     // samples per wave
 
-__device__ __forceinline__ void merge_pair_wave(const float* tA, const int* iA, int nA,
-                                                const float* tB, const int* iB, int nB,
-                                                float* to, int* io, int32_t* gout) {
+// Sample ids in LDS are u16 positions in the ray's staged runs (model k's run
+// starts at kb[k]); the last level maps them to global sample indices
+// (ko[k] + id - kb[k]).  u16 ids take a block to 48 KB of LDS: 3 blocks (6
+// waves) per CU instead of 2, for a latency-bound merge.
+__device__ __forceinline__ void merge_pair_wave(const float* tA, const uint16_t* iA, int nA,
+                                                const float* tB, const uint16_t* iB, int nB,
+                                                float* to, uint16_t* io, int32_t* gout,
+                                                const int* kb, const int* ko, int K) {
     const int lane = rn_lane();
     const int n = nA + nB;
     const int L = (n + RN_WAVE - 1) / RN_WAVE;
@@ -1939,8 +1944,16 @@ __device__ __forceinline__ void merge_pair_wave(const float* tA, const int* iA, 
     for (int q = d; q < e; ++q) {
         const bool takeA = a < nA && (b >= nB || tA[a] <= tB[b]);
         const int idx = takeA ? iA[a] : iB[b];
-        if (gout) gout[q] = idx;
-        else { to[q] = takeA ? tA[a] : tB[b]; io[q] = idx; }
+        if (gout) {
+            int base = ko[0];
+#pragma unroll
+            for (int j = 1; j < MB_KMAX; ++j)
+                if (j < K && idx >= kb[j]) base = ko[j] - kb[j];
+            gout[q] = base + idx;
+        } else {
+            to[q] = takeA ? tA[a] : tB[b];
+            io[q] = (uint16_t)idx;
+        }
         a += takeA ? 1 : 0;
         b += takeA ? 0 : 1;
     }
@@ -1952,7 +1965,8 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
                  const int32_t* __restrict__ seg_count, const float* __restrict__ ts,
                  int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
     __shared__ float sT[PLANM_WAVES][2][PLANM_LDS];
-    __shared__ int sI[PLANM_WAVES][2][PLANM_LDS];
+    __shared__ uint16_t sI[PLANM_WAVES][2][PLANM_LDS];
+    static_assert(PLANM_LDS <= 65536, "u16 sample ids");
     const int wid = threadIdx.x / RN_WAVE;
     const int r = blockIdx.x * PLANM_WAVES + wid;
     if (r >= B) return;                      // wave-uniform; no block barrier below
@@ -1997,10 +2011,13 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
         return;
     }
     int cur = 0;
+    int kb[MB_KMAX];                          // the models' runs (bnd is merged below)
+#pragma unroll
+    for (int k = 0; k < MB_KMAX; ++k) kb[k] = k < K ? bnd[k] : 0;
     for (int k = 0; k < K; ++k)
         for (int i = lane; i < bnd[k + 1] - bnd[k]; i += RN_WAVE) {
             sT[wid][0][bnd[k] + i] = ts[off[k] + i];
-            sI[wid][0][bnd[k] + i] = off[k] + i;
+            sI[wid][0][bnd[k] + i] = (uint16_t)(bnd[k] + i);
         }
     int nr = K;
     while (true) {
@@ -2008,12 +2025,12 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         const bool last = nr <= 2;
         const float* ts_ = sT[wid][cur];
-        const int* is_ = sI[wid][cur];
+        const uint16_t* is_ = sI[wid][cur];
         for (int p = 0; 2 * p < nr; ++p) {
             const int a0 = bnd[2 * p], a1 = bnd[min(2 * p + 1, nr)], b1 = bnd[min(2 * p + 2, nr)];
             merge_pair_wave(ts_ + a0, is_ + a0, a1 - a0, ts_ + a1, is_ + a1, b1 - a1,
                             sT[wid][cur ^ 1] + a0, sI[wid][cur ^ 1] + a0,
-                            last ? perm + ms + a0 : nullptr);
+                            last ? perm + ms + a0 : nullptr, kb, off, K);
         }
         if (last) return;
         // runs after this level: boundaries of the merged pairs

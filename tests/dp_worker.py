@@ -56,20 +56,28 @@ def main(out_path):
     step(r, o, d, nz, sd, bg, ar.views)
     ar.reduce()
     torch.cuda.synchronize()
-    reduced = ar.flat.clone()
+    result = ar.flat.clone()
     # the staged form bench.py uses over RCCL (comm stream, events, the MLP +
-    # gate bucket then the grid in 4 buckets), forced here over gloo: the same
-    # averaged buffer, and its timing fields
+    # gate bucket then the grid in 4 buckets), forced here over gloo, on one
+    # more step's local gradient: the same averaged buffer as reduce() of the
+    # same gradient, and its timing fields
     ar.zero()
     ar.reset_timing()
     step(r, o, d, nz, sd, bg, ar.views)
+    torch.cuda.synchronize()
+    local = ar.flat.clone()
     hs = [ar.launch_range(*ar.param_range(1), 1, stream_ordered=True),
           ar.launch_range(*ar.param_range(0, 1), 4, stream_ordered=True)]
     for h in hs:
         ar.finish(h)
     torch.cuda.synchronize()
-    staged_equal = bool(torch.equal(ar.flat, reduced))
+    staged = ar.flat.clone()
     stats = ar.comm_stats(1)
+    ar.flat.copy_(local)
+    ar.reduce()
+    torch.cuda.synchronize()
+    staged_equal = bool(torch.equal(staged, ar.flat))
+    ar.flat.copy_(result)
     if rank == 0:
         ref = rdist.GradAllReduce(params, dev)      # not reduced: a local buffer
         ref.zero()
