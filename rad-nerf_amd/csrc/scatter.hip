@@ -155,7 +155,7 @@ template <int ABL, bool PROF = false, int BIS = 0>
 __global__ void __launch_bounds__(GB_SUM_THREADS, 8)   // two workgroups per CU
 k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t* __restrict__ redo,
            float* __restrict__ grad) {
-    extern __shared__ int64_t acc[];               // [GB_SLICE][2]
+    extern __shared__ int64_t acc[];               // [GB_SLICE][2], then the group counter
     uint64_t tp = PROF ? __builtin_amdgcn_s_memtime() : 0, cyc[4] = {0, 0, 0, 0}, ngrp = 0;
     const uint64_t rt0 = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     if (redo && __builtin_nontemporal_load(redo) != 0) return;   // the fp32 redo replaces the step
@@ -167,91 +167,105 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     const uint32_t npg = min(__builtin_nontemporal_load(&P.ctl->level_npages[l]), P.pool_pages);
     const float sc = scale[l];
     if (npg == 0u || sc == 0.f) return;            // no records (an fp32 level went in by atomics)
-    const int tid = threadIdx.x, lane = rn_lane(), wid = tid / RN_WAVE;
+    const int tid = threadIdx.x, lane = rn_lane();
     const uint32_t sbits = P.slice_bits[l], emask = (1u << sbits) - 1u;
     for (int i = tid; i < (2 << sbits); i += GB_SUM_THREADS) acc[i] = 0;
+    if (tid == 0) *reinterpret_cast<uint32_t*>(acc + 2 * GB_SLICE) = 0u;   // the group counter
     __syncthreads();
     auto stamp = [&](int ph) {
         if (PROF) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[ph] += t - tp; tp = t; }
     };
     stamp(0);
     const uint32_t* lp = P.level_pages + (size_t)l * P.pool_pages;
-    constexpr uint32_t NW = GB_SUM_THREADS / RN_WAVE;
-    // A batch is 64 pages per wave: lane i of wave w holds the run of this
-    // slice (page, start | count << 16) of list entry base + (i / 8) * NW * 8 +
-    // w * 8 + i % 8 (groups of 8 pages dealt round-robin to the waves, so a
-    // level's last, partial batch still spreads over all of them); the next
-    // batch's runs are loaded while this one is summed.  The slices of a level
-    // walk its page list from different starting points (slice b at
-    // b / nslices of the list).
+    // Each wave takes groups of 8 pages of the level's list from a workgroup
+    // counter (lanes 0-7 hold a group's runs of this slice: page, start |
+    // count << 16) and loads the next group's runs while it sums this one.
+    // Dealing the groups statically (wave w: groups w, w + 16, ...) left ~20 %
+    // of the waves' time at the final barrier, waiting for the slowest wave
+    // (memory latency varies from group to group): 0.74 against 0.68 ms at
+    // C5's volume (profiles/r04/binprobe/binprobe_full_dy.json, bis5).  The
+    // slices of a level walk its page list from different starting points
+    // (slice b at b / nslices of the list).
     const uint32_t nsl = s.first[q + 1] - s.first[q];
     const uint32_t start = (uint32_t)(((uint64_t)b * npg) / nsl);
-    auto runs_of = [&](uint32_t base, uint32_t& pg, uint32_t& d) {
-        uint32_t i = base + (lane >> 3) * (NW * GB_RUNS) + wid * GB_RUNS + (lane & 7);
-        pg = 0u; d = 0u;
-        if (i < npg) {
-            i += start;
-            i = i >= npg ? i - npg : i;
-            pg = lp[i];
-            d = P.desc[(size_t)pg * GB_MAX_BINS + b];
+    uint64_t fold = 0ull;
+    // the runs of one group of 8 pages: lanes k0 .. k0 + 7 of (pgc, dc)
+    auto sum_group = [&](uint32_t pgc, uint32_t dc, int k0) {
+        ngrp += PROF ? 1 : 0;
+        uint64_t r0[GB_RUNS], r1[GB_RUNS];
+        uint32_t cnt[GB_RUNS], st[GB_RUNS];
+        const uint64_t* pgp[GB_RUNS];
+#pragma unroll
+        for (int j = 0; j < GB_RUNS; ++j) {
+            const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
+            const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
+            // BIS (timing bisection only, full-lane loads): 1 load every run,
+            // 2 and fold every lane, 3 every run 64 records, 4 as built
+            // before round 4's exec-masked loads
+            cnt[j] = BIS == 3 ? 64u : dk >> 16;
+            st[j] = dk & 0xffffu;
+            pgp[j] = P.pages_out + (size_t)pk * GB_PAGE;
+            r0[j] = 0ull; r1[j] = 0ull;
+            if (BIS == 0) {                                 // the run's lanes only
+                if ((uint32_t)lane < cnt[j])
+                    r0[j] = __builtin_nontemporal_load(pgp[j] + st[j] + lane);
+                if ((uint32_t)lane + 64u < cnt[j])
+                    r1[j] = __builtin_nontemporal_load(pgp[j] + st[j] + 64u + lane);
+            } else {                                        // full-lane loads (timing)
+                if (BIS != 4 || cnt[j] != 0u)
+                    r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
+                if (cnt[j] > 64u)
+                    r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < GB_RUNS; ++j) {
+            if (BIS == 2 || (uint32_t)lane < cnt[j]) gb_add<ABL>(acc, r0[j], fold, emask);
+            if ((uint32_t)lane + 64u < cnt[j]) gb_add<ABL>(acc, r1[j], fold, emask);
+            // the rest of a run over 128 records (the coarse levels' runs are
+            // long): 8 full-lane loads in flight per step
+            for (uint32_t o = 128u; o < cnt[j]; o += 8u * 64u) {
+                uint64_t rr[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    rr[u] = 0ull;
+                    if (BIS == 0 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
+                        rr[u] = __builtin_nontemporal_load(
+                            pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (o + 64u * u + lane < cnt[j]) gb_add<ABL>(acc, rr[u], fold, emask);
+            }
         }
     };
-    uint32_t pg, d;
-    uint64_t fold = 0ull;
-    runs_of(0u, pg, d);
-    if (PROF) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); stamp(1); }
-    for (uint32_t base = 0u; base < npg; base += NW * 64u) {
-        const uint32_t pgc = pg, dc = d;
-        runs_of(base + NW * 64u, pg, d);
-#pragma unroll 1
-        for (int k0 = 0; k0 < 64; k0 += GB_RUNS) {
-            ngrp += PROF ? 1 : 0;
-            uint64_t r0[GB_RUNS], r1[GB_RUNS];
-            uint32_t cnt[GB_RUNS], st[GB_RUNS];
-            const uint64_t* pgp[GB_RUNS];
-#pragma unroll
-            for (int j = 0; j < GB_RUNS; ++j) {
-                const uint32_t dk = (uint32_t)__builtin_amdgcn_readlane((int)dc, k0 + j);
-                const uint32_t pk = (uint32_t)__builtin_amdgcn_readlane((int)pgc, k0 + j);
-                // BIS (timing bisection only, full-lane loads): 1 load every run,
-                // 2 and fold every lane, 3 every run 64 records, 4 as built
-                // before round 4's exec-masked loads
-                cnt[j] = BIS == 3 ? 64u : dk >> 16;
-                st[j] = dk & 0xffffu;
-                pgp[j] = P.pages_out + (size_t)pk * GB_PAGE;
-                r0[j] = 0ull; r1[j] = 0ull;
-                if (BIS == 0) {                                 // the run's lanes only
-                    if ((uint32_t)lane < cnt[j])
-                        r0[j] = __builtin_nontemporal_load(pgp[j] + st[j] + lane);
-                    if ((uint32_t)lane + 64u < cnt[j])
-                        r1[j] = __builtin_nontemporal_load(pgp[j] + st[j] + 64u + lane);
-                } else {                                        // full-lane loads (timing)
-                    if (BIS != 4 || cnt[j] != 0u)
-                        r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
-                    if (cnt[j] > 64u)
-                        r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
-                }
+    {
+        uint32_t* ctr = reinterpret_cast<uint32_t*>(acc + 2 * GB_SLICE);
+        const uint32_t ngr = (npg + GB_RUNS - 1u) / GB_RUNS;
+        auto grab = [&]() -> uint32_t {
+            uint32_t x = 0u;
+            if (lane == 0) x = atomicAdd(ctr, 1u);
+            return (uint32_t)__builtin_amdgcn_readfirstlane((int)x);
+        };
+        auto group_runs = [&](uint32_t g, uint32_t& pg, uint32_t& d) {
+            uint32_t i = g * GB_RUNS + (uint32_t)(lane & 7);
+            pg = 0u; d = 0u;
+            if (lane < GB_RUNS && g < ngr && i < npg) {
+                i += start;
+                i = i >= npg ? i - npg : i;
+                pg = lp[i];
+                d = P.desc[(size_t)pg * GB_MAX_BINS + b];
             }
-#pragma unroll
-            for (int j = 0; j < GB_RUNS; ++j) {
-                if (BIS == 2 || (uint32_t)lane < cnt[j]) gb_add<ABL>(acc, r0[j], fold, emask);
-                if ((uint32_t)lane + 64u < cnt[j]) gb_add<ABL>(acc, r1[j], fold, emask);
-                // the rest of a run over 128 records (the coarse levels' runs are
-                // long): 8 full-lane loads in flight per step
-                for (uint32_t o = 128u; o < cnt[j]; o += 8u * 64u) {
-                    uint64_t rr[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) {
-                        rr[u] = 0ull;
-                        if (BIS == 0 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
-                            rr[u] = __builtin_nontemporal_load(
-                                pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
-                    }
-#pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        if (o + 64u * u + lane < cnt[j]) gb_add<ABL>(acc, rr[u], fold, emask);
-                }
-            }
+        };
+        uint32_t g = grab(), pg, d;
+        group_runs(g, pg, d);
+        if (PROF) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); stamp(1); }
+        while (g < ngr) {                               // wave-uniform
+            const uint32_t pgc = pg, dc = d;
+            const uint32_t gn = grab();
+            group_runs(gn, pg, d);
+            sum_group(pgc, dc, 0);
+            g = gn;
         }
     }
     stamp(2);
@@ -355,7 +369,7 @@ int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const
     P.ctl = (GbCtl*)ctl; P.desc = (uint32_t*)desc; P.level_pages = (uint32_t*)level_pages;
     P.pages_out = (uint64_t*)pages_out; P.pool_pages = (uint32_t)pool_pages;
     for (int l = 0; l < RN_L; ++l) P.slice_bits[l] = (uint8_t)gb_slice_bits(level_hsize[l]);
-    const size_t lds = (size_t)GB_SLICE * 2 * sizeof(int64_t);
+    const size_t lds = (size_t)GB_SLICE * 2 * sizeof(int64_t) + 16;   // + the group counter
     // ablations (timing studies only): bit 16 no LDS adds, bit 21 per-phase cycles
     const int dbg = rn_debug_flags_internal() >> 16;
     hipStream_t st = (hipStream_t)stream;
