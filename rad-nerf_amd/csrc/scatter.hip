@@ -182,8 +182,9 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
     // count << 16) and loads the next group's runs while it sums this one.
     // Dealing the groups statically (wave w: groups w, w + 16, ...) left ~20 %
     // of the waves' time at the final barrier, waiting for the slowest wave
-    // (memory latency varies from group to group): 0.74 against 0.68 ms at
-    // C5's volume (profiles/r04/binprobe/binprobe_full_dy.json, bis5).  The
+    // (memory latency varies from group to group): at 1/8 of C5's volume
+    // 0.139 -> 0.118 ms, at the full volume 0.74 -> 0.73-0.74 ms
+    // (profiles/r04/binprobe/binprobe_{fp,full}_dy*.json).  The
     // slices of a level walk its page list from different starting points
     // (slice b at b / nslices of the list).
     const uint32_t nsl = s.first[q + 1] - s.first[q];
