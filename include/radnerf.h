@@ -298,6 +298,8 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
 int rn_debug_gb_cycles(unsigned long long* out);
 int rn_grid_bin_layout(int32_t* out);   /* host: page records, bins per page, slice
                                           entries, ctl bytes, index bits, value bits */
+int rn_grid_slice_bits(const uint32_t* level_hsize, int32_t* out);   /* host: log2 of each
+                                          level's slice size (out [16]) */
 int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
                 const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
                 uint32_t* level_pages, int32_t pool_pages, int32_t blocks, void* stream);

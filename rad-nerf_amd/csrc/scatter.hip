@@ -318,6 +318,16 @@ int rn_grid_bin_layout(int32_t* out) {
     return 0;
 }
 
+int rn_grid_slice_bits(const uint32_t* level_hsize, int32_t* out) {
+    RN_CHECK_ARG(level_hsize && out, "null pointer");
+    for (int l = 0; l < RN_L; ++l) {
+        RN_CHECK_ARG(level_hsize[l] >= 1 && level_hsize[l] <= (1u << GB_IDX_BITS),
+                     "level too large for binning");
+        out[l] = (int32_t)gb_slice_bits(level_hsize[l]);
+    }
+    return 0;
+}
+
 int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
                 const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
                 uint32_t* level_pages, int32_t pool_pages, int32_t blocks, void* stream) {

@@ -61,6 +61,7 @@ SIGNATURES = {
     "rn_grid_fx_fold": [P, P, P, P, P, P, P, P, P, P],
     "rn_grid_bin_layout": [P],
     "rn_debug_gb_cycles": [P],
+    "rn_grid_slice_bits": [P, P],
     "rn_grid_bin": [P, P, P, P, P, P, P, I32, I32, P],
     "rn_grid_sum": [P, P, P, P, P, P, I32, P, P, P, P],
     "rn_grid_binned_fold": [P, P, P, P, P, P, P, P, I32, P, P, P, P, P, P],

@@ -78,3 +78,25 @@ def test_grid_bin_and_sum_reject_oversized_levels():
     off = np.zeros(16, np.uint32)
     with pytest.raises(RuntimeError, match="level too large"):
         L.grid_sum(off.ctypes.data, hs.ctypes.data, *[V] * 4, 16, V, None, V, None)
+
+
+def test_grid_slice_bits_rule():
+    """rn_grid_slice_bits (host): each level's slice is the smallest power of
+    two >= 64 entries that cuts the level into <= 128 slices, 4096 at most
+    (csrc/rn_bin.h gb_slice_bits, used by the bin and sum passes)."""
+    import numpy as np
+
+    from radnerf_amd import layout as LY
+    L = _lib.lib()
+    for scale in (0.5, 16.0):
+        hs = np.ascontiguousarray(LY.grid_levels(scale)["hsize"], dtype=np.uint32)
+        out = np.zeros(16, np.int32)
+        L.grid_slice_bits(hs.ctypes.data, out.ctypes.data)
+        for h, b in zip(hs.tolist(), out.tolist()):
+            assert 6 <= b <= 12, (scale, h, b)
+            assert -(-h // (1 << b)) <= 128 or b == 12, (scale, h, b)
+            assert b == 6 or -(-h // (1 << (b - 1))) > 128, (scale, h, b)
+        if scale == 16.0:
+            assert out[0] == 6 and out[-1] == 12     # 4096 entries in 64s; 2^19 in 4096s
+    with pytest.raises(RuntimeError, match="level too large"):
+        L.grid_slice_bits(np.full(16, 1 << 21, np.uint32).ctypes.data, np.zeros(16, np.int32).ctypes.data)
