@@ -145,6 +145,9 @@ def parse():
     ap.add_argument("--buckets", type=int, default=4,
                     help="N>1: the gradient all-reduce as this many asynchronous bucket "
                          "collectives, each averaged behind its own wait (1 = one collective)")
+    ap.add_argument("--grid-split", type=int, default=8,
+                    help="N>1, binned fold: the grid levels [this, 16) are summed first and "
+                         "their all-reduce starts while levels [0, this) are summed")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the world size, print the ranks seen and exit "
                          "(no GPU work; with --backend gloo it runs on CPU)")
@@ -203,14 +206,22 @@ def launch_check(args, rank, local, world):
         n_grid = 2 * int(LY.grid_levels(0.5)["n_entries"])
         ar = rdist.GradAllReduce([torch.zeros(n_grid), torch.zeros(2, LY.FIELD_PARAMS),
                                   torch.zeros(LY.gate_params(2))], "cpu")
-        for v in ar.views:
-            v.fill_(float(rank + 1))
-        hs = [ar.launch_range(*ar.param_range(1), 1),
-              ar.launch_range(*ar.param_range(0, 1), args.buckets)]
+        for i, v in enumerate(ar.views):
+            v.copy_(torch.randn(v.shape, generator=torch.Generator().manual_seed(rank * 10 + i)))
+        local = ar.flat.clone()
+        # the step's schedule: MLP + gate, the fine levels, the coarse levels
+        rg = rdist.step_ranges(ar, LY.grid_levels(0.5)["offset"], args.grid_split)
+        hs = [ar.launch_range(*rg["rest"], 1), ar.launch_range(*rg["fine"], args.buckets),
+              ar.launch_range(*rg["coarse"], 1)]
         for h in hs:
             ar.finish(h)
         comm = ar.comm_stats(1)
-        comm["mean_ok"] = bool(torch.all(ar.flat == (world + 1) / 2))
+        # the same local gradients through one plain all-reduce: bit-identical
+        ref = local.clone()
+        dist.all_reduce(ref)
+        ref.div_(world)
+        comm["mean_ok"] = bool(torch.equal(ar.flat, ref))
+        comm["ranges"] = {k: list(v) for k, v in rg.items()}
         comm["backend"] = dist.get_backend()
     if rank == 0:
         print(json.dumps({"launch_check": True, "n_gpus": world,
@@ -292,9 +303,11 @@ def main():
     # as field_bwd has written them, beside the grid gradient's fold (or bin
     # + sum); the grid gradient in args.buckets buckets after the backward.
     # Both on a comm stream, bracketed by events there (comm fields below).
-    grid_rng, rest_rng = ar.param_range(0, 1), ar.param_range(1)
+    r.grid_split_level = args.grid_split
+    rng = rdist.step_ranges(ar, model.xyz_encoder.h_offset, r.grid_split_level)
     comm_on = [world > 1]
     pending = []
+    grid_early = [None]             # the grid range already launched this step
     # gloo's collectives on device tensors block the host until they complete:
     # launched from inside the backward they stall the launch queue mid-step
     # (the 2-rank gloo rehearsal on one GPU fell from 476 to 80 Msamples/s),
@@ -305,20 +318,34 @@ def main():
         if comm_on[0] and early_ok:
             main = torch.cuda.current_stream(dev)
             main.wait_stream(r._side(dev))       # the gate backward ran on the side stream
-            pending.append(ar.launch_range(*rest_rng, 1))
+            pending.append(ar.launch_range(*rng["rest"], 1))
+
+    def grid_levels_ready(split):
+        # binned fold: levels [split, 16) are summed, [0, split) not yet (split
+        # 0: the whole grid is final) -- their collective overlaps the rest
+        if comm_on[0] and early_ok:
+            a, b = rdist.step_ranges(ar, model.xyz_encoder.h_offset, split)["fine"]
+            pending.append(ar.launch_range(a, b, args.buckets))
+            grid_early[0] = a
 
     r.after_field_bwd = early_bucket
+    r.after_grid_levels = grid_levels_ready
 
     def step(i):
         ar.zero()
         _, _, _, gt, _ = r.forward(rays_o, rays_d, rays_d, noises[i % 4], bg, 1e-4, esf)
         samples_acc.add_(r.ws.meta[1])
+        grid_early[0] = None
         r.backward(rays_o, rays_d, rays_d, gt, bg, g_rgb, g_op, g_depth, None, 1e-4,
                    grid_grad=ar.views[0], mlp_grad=ar.views[1], gate_grad=ar.views[2])
         if comm_on[0]:
             if not pending:                      # (no merged backward: no early bucket)
-                pending.append(ar.launch_range(*rest_rng, 1))
-            pending.append(ar.launch_range(*grid_rng, args.buckets))
+                pending.append(ar.launch_range(*rng["rest"], 1))
+            g0, g1 = ar.param_range(0, 1)
+            if grid_early[0] is None:            # gloo: the whole grid after the backward
+                pending.append(ar.launch_range(g0, g1, args.buckets))
+            elif grid_early[0] > g0:             # the coarse levels, summed last
+                pending.append(ar.launch_range(g0, grid_early[0], 1))
             for h in pending:                    # pinned: partial gradients add up
                 ar.finish(h, average=not args.pinned)
             pending.clear()
@@ -366,8 +393,11 @@ def main():
             "ms_per_step_without": round(float(no_comm) / args.steps * 1e3, 4),
             "exposed_ms": round((float(with_comm) - float(no_comm)) / args.steps * 1e3, 4),
             "backend": dist.get_backend(),
-            "schedule": ("MLP+gate bucket after field_bwd (beside the grid fold), grid in "
-                         f"{args.buckets} buckets after the backward; comm stream events"
+            "schedule": ("MLP+gate bucket after field_bwd (beside the grid fold); binned fold: "
+                         f"grid levels [{args.grid_split}, 16) in {args.buckets} buckets once "
+                         "summed (beside the coarse levels' sum), levels "
+                         f"[0, {args.grid_split}) after it; int32 fold: the grid in "
+                         f"{args.buckets} buckets after the fold; comm stream events"
                          if early_ok else
                          f"gloo: MLP+gate bucket and the grid in {args.buckets} buckets after the "
                          "backward (host-blocking collectives); comm stream events")})
@@ -571,6 +601,8 @@ def main():
 
     # per-kernel breakdown (rank 0) and the roofline of the dominant kernel
     kms = {k: float(np.mean(v)) for k, v in kt.items()}
+    if "fx_bin" in kms:             # binned fold: bin + check, then the sums (redo between)
+        kms["fx_fold"] = kms["fx_bin"] + kms.get("fx_sum", 0.0)
     samples_per_step_rank = int(samples_acc) / args.steps
     bwd_ms = kms.get("field_bwd", float("nan"))
     achieved = samples_per_step_rank * FIELD_BWD_BYTES_PER_SAMPLE / (bwd_ms * 1e-3) / 1e9

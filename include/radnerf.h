@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 3   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 4   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -265,8 +265,8 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * scatter, no dW): it returns at once unless *fx_redo is set; and swaps
  * fx_scale_cur / fx_scale_next for the next step.
  * fx_mode 0: fp32 atomics (and the optional igrad_* integer mode).
- * fx_mode 4: binned (rn_grid_bin below): the fixed-point records (int22, the
- * largest < 2^18 units) are appended to the gb_* page pool (gb_ctl is reset
+ * fx_mode 4: binned (rn_grid_bin below): the fixed-point records (e5m17, the
+ * largest < 2^38 units) are appended to the gb_* page pool (gb_ctl is reset
  * by the call) instead of atomically added; rn_grid_binned_fold then bins
  * and sums them into grid_grad (fx_acc unused).                            */
 int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
@@ -277,10 +277,14 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
 /* Binned ("store and sum") grid-gradient scatter, passes 2 and 3
  * (scatter.hip, formats in csrc/rn_bin.h).  Pass 1 is rn_field_bwd_merged
  * with fx_mode 4: it appends each level's fixed-point records (u64: entry
- * index 20 bits, two int22 features) to 64-KB pages of a pool instead of
- * issuing memory-side atomics.  ctl: the 128-B GbCtl block (pages taken,
- * pages per level), zero before pass 1; page_meta [pool_pages] u32 (level |
- * count << 8); pages_in / pages_out [pool_pages][8192] u64; desc
+ * index 20 bits, two 22-bit e5m17 features, rn_grid_record_encode) to 64-KB
+ * pages of a pool instead of issuing memory-side atomics.  ctl: the 128-B
+ * GbCtl block (u32 pages taken, u32 pages per level [16], u32 fault bits:
+ * 1 a page meta with a level >= 16 or more than 8192 records, 2 a record
+ * index outside its level, 4 a level list past the pool, 8 a page id or run
+ * outside the pool / page -- refused, never followed), zero before pass 1;
+ * page_meta [pool_pages] u32 (level | count << 8); pages_in / pages_out
+ * [pool_pages][8192] u64; desc
  * [pool_pages][256] u32; level_pages [16][pool_pages] u32.
  * rn_grid_bin sorts each page by slice of its level (level_hsize [16]: a
  * slice is the smallest power of two >= 64 entries that cuts the level into
@@ -297,25 +301,43 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
  * earliest start / latest end (s_memrealtime ticks, 100 MHz) */
 int rn_debug_gb_cycles(unsigned long long* out);
 int rn_grid_bin_layout(int32_t* out);   /* host: page records, bins per page, slice
-                                          entries, ctl bytes, index bits, value bits */
+                                          entries, ctl bytes, index bits, value bits,
+                                          mantissa bits, target bits (out [8]) */
 int rn_grid_slice_bits(const uint32_t* level_hsize, int32_t* out);   /* host: log2 of each
                                           level's slice size (out [16]) */
+/* host: a record value x (gradient * 2^e_l) as the walk stores it, e5m17:
+ * bits [0, 17) a two's-complement mantissa m, [17, 22) an exponent e, value
+ * m * 2^e (e = 0 and m = rint(x) below 2^15; else |m| in [2^14, 2^15]), and
+ * back (decode: the exact int64 value the sum pass adds) */
+int rn_grid_record_encode(const float* x, int64_t n, uint32_t* out);
+int rn_grid_record_decode(const uint32_t* f, int64_t n, int64_t* out);
 int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
                 const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
                 uint32_t* level_pages, int32_t pool_pages, int32_t blocks, void* stream);
-/* rn_grid_bin + the binned redo / scale check (a record at 2^21 units, a
- * non-finite one, or a pool overflow sets *fx_redo; next scales 2^(18 - e))
+/* rn_grid_bin + the binned redo / scale check (a record at 2^46 units, a
+ * non-finite one, a pool overflow or a bin-pass fault sets *fx_redo; next
+ * scales 2^(38 - e))
  * + rn_grid_sum, for a fx_mode 4 backward; the caller then launches the
  * fx_mode 3 redo exactly as after rn_grid_fx_fold.                         */
+/* the first two steps of rn_grid_binned_fold (bin + check); a caller that
+ * overlaps the grid gradient's all-reduce with the sum pass then runs
+ * rn_grid_sum over the fine levels, starts their collective, and runs it
+ * over the coarse ones (the fx_mode 3 redo may go before the sums: they exit
+ * at once when *fx_redo is set) */
+int rn_grid_bin_check(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
+                      const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
+                      uint32_t* level_pages, int32_t pool_pages, const float* fx_scale_cur,
+                      float* fx_scale_next, uint32_t* fx_stats, int32_t* fx_redo, void* stream);
 int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsize, void* ctl,
                         const uint32_t* page_meta, const uint64_t* pages_in, uint64_t* pages_out,
                         uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
                         const float* fx_scale_cur, float* fx_scale_next, uint32_t* fx_stats,
                         int32_t* fx_redo, float* grid_grad, void* stream);
+/* levels [level_lo, level_hi) only (0, 16: all) */
 int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const void* ctl,
                 const uint32_t* desc, const uint32_t* level_pages, const uint64_t* pages_out,
                 int32_t pool_pages, const float* fx_scale, const int32_t* redo, float* grid_grad,
-                void* stream);
+                int32_t level_lo, int32_t level_hi, void* stream);
 
 /* Fused test-time render (ml_rendering.py:81-155 / rendering.py:113-189,
  * raymarching.cu:335-404, volumerendering.cu:206-286): one wave per ray marches

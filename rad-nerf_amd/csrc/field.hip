@@ -140,7 +140,7 @@ __device__ __forceinline__ void ring_issue(ScatterRing& R, int s, uint32_t cnt,
         const uint32_t* base = R.ring + s * 3 * SC_RING;
         const uint32_t off = base[rec] + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * SC_RING + rec];
-        if (dbg & 1) asm volatile("" :: "v"(off), "v"(v));
+        if (rn_dbg(dbg) & 1) asm volatile("" :: "v"(off), "v"(v));
         else __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
                                                              (int)off, 0, 0);
     }
@@ -441,11 +441,11 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         const uint32_t* base = W.ring + s * 3 * W2_RING;
         const uint32_t off = base[rec] + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
-        if (dbg & 1) {
+        if (rn_dbg(dbg) & 1) {
             asm volatile("" :: "v"(off), "v"(v));
         } else if (GM == 3 && !fx_lvl) {
             // redo: this level went in with fp32 atomics in the first pass
-        } else if (dbg & 64) {      // ablation: non-returning i32 adds (timing only)
+        } else if (rn_dbg(dbg) & 64) {      // ablation: non-returning i32 adds (timing only)
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
                 (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
         } else if (GM == 4 && fx_lvl) {
@@ -454,9 +454,9 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             // r's low word, lane 2r + 1 its high word
             const uint32_t ab = v & 0x7fffffffu;
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
-            int q;
-            asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
-            q = min(max(q, -GB_V_MAX), GB_V_MAX);         // larger records: vmax flags a redo
+            // e5m17 (rn_bin.h); a record at or past 2^46 units saturates and
+            // vmax flags the step for the fp32 redo
+            const int q = (int)gb_encode(__uint_as_float(v) * sc_s);
             const int qp = __builtin_amdgcn_mov_dpp(q, 0xb1, 0xf, 0xf, true);   // partner lane ^ 1
             const uint32_t idx = (base[rec] >> 3) - (odd ? W.loffB : W.loffA);
             const uint32_t q0 = (uint32_t)((lane & 1) ? qp : q), q1 = (uint32_t)((lane & 1) ? q : qp);
@@ -466,7 +466,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             const uint32_t pg = odd ? W.pgB : W.pgA, n = odd ? W.nB : W.nA;
             uint32_t* dst = reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane;
             if (pg < G.pool_pages) {
-                if (dbg & 8) *dst = word;                // (timing only: plain stores)
+                if (rn_dbg(dbg) & 8) *dst = word;                // (timing only: plain stores)
                 else __builtin_nontemporal_store(word, dst);
             }
         } else if (GM == 2 && fx_lvl) {
@@ -690,14 +690,28 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
     walk_end(a, sT, R, grad_rs, W, a.dbg);
 }
 
-// dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32)
+// dW tile over the 8 waves' images: dY features [ya,+32) x X features [xa,+32).
+// Software-pipelined: the four transposed LDS reads of step j + DW_DEPTH - 1
+// are issued before step j's MFMA, so each MFMA waits only for its own
+// operands (lgkmcnt counts in issue order).  Written as one load per step
+// followed by its MFMA, the compiler waited lgkmcnt(0) before every MFMA and
+// the 16-step tile took 16 LDS round trips (round 5, field.hip ISA).
+#define DW_DEPTH 3
 __device__ __forceinline__ f32x16 dw_block_tile(const rn_half* sImg, int ya, int xa, f32x16 acc) {
+    constexpr int NS = 2 * BWD_WAVES;                 // 16 steps of 16 samples
+    half8 ys[DW_DEPTH], xs[DW_DEPTH];
+    auto load = [&](int j, half8& y, half8& x) {
+        const rn_half* iy = sImg + (j >> 1) * 2 * RN_IMG_HALFS;
+        y = rn_img_read(iy, ya, j & 1);
+        x = rn_img_read(iy + RN_IMG_HALFS, xa, j & 1);
+    };
 #pragma unroll
-    for (int w = 0; w < BWD_WAVES; ++w) {
-        const rn_half* iy = sImg + w * 2 * RN_IMG_HALFS;
-        const rn_half* ix = iy + RN_IMG_HALFS;
-        acc = rn_mfma(rn_img_read(iy, ya, 0), rn_img_read(ix, xa, 0), acc);
-        acc = rn_mfma(rn_img_read(iy, ya, 1), rn_img_read(ix, xa, 1), acc);
+    for (int j = 0; j < DW_DEPTH - 1; ++j) load(j, ys[j], xs[j]);
+#pragma unroll
+    for (int j = 0; j < NS; ++j) {
+        if (j + DW_DEPTH - 1 < NS)
+            load(j + DW_DEPTH - 1, ys[(j + DW_DEPTH - 1) % DW_DEPTH], xs[(j + DW_DEPTH - 1) % DW_DEPTH]);
+        acc = rn_mfma(ys[j % DW_DEPTH], xs[j % DW_DEPTH], acc);
     }
     return acc;
 }
@@ -919,7 +933,7 @@ k_field_bwd(FieldArgs a) {
     rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
     rn_half* imgX = imgY + RN_IMG_HALFS;
     const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
-    const bool do_dw = !(a.dbg & 2);
+    const bool do_dw = !(rn_dbg(a.dbg) & 2);
 
     // owned dW tiles (ownership table in the header comment above):
     //   w0: r3(n=0), g2(n=0)   w1: r3(n=1), g2(n=1)   w2..w5: r2(m,n)
@@ -927,7 +941,7 @@ k_field_bwd(FieldArgs a) {
     f32x16 accA = rn_zero16(), accB = rn_zero16();
     DwScale cur = {0.f, 0.f};   // scales the accumulators are expressed at (0 = empty)
 
-    const bool do_sc = !(a.dbg & 4);
+    const bool do_sc = !(rn_dbg(a.dbg) & 4);
     // scatter staging (dL/dfeature rows, unit coords of the iteration's 256
     // samples) reuses the image region, free between B10 and the next B0
     float* sG = reinterpret_cast<float*>(sImg);                        // [256][SG_STRIDE]
@@ -1065,7 +1079,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     rn_half* imgX = imgY + RN_IMG_HALFS;
     const __amdgpu_buffer_rsrc_t grad_rs = rn_rsrc(a.grid_grad, 2 * a.grid_bytes);
     const int dbg = ABL ? a.dbg : 0;      // ablation flags (tools/ablate.py) only in ABL builds
-    const bool do_dw = !(dbg & 2) && GM != 3;
+    const bool do_dw = !(rn_dbg(dbg) & 2) && GM != 3;
     // fixed point: this wave's two levels' scales (wave-uniform) and maxima
     float fxA = 0.f, fxB = 0.f;
     uint32_t vmA = 0u, vmB = 0u;
@@ -1077,7 +1091,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
         fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
     }
-    const bool do_sc = !(dbg & 4);
+    const bool do_sc = !(rn_dbg(dbg) & 4);
     // walk windows of MB_WIN rows per eighth: each window's staging loads
     // wait (vmcnt, in issue order) for the atomics the previous window issued,
     // so fewer, longer windows wait less often (round 3: 32 -> 64)
@@ -1105,7 +1119,11 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     f32x16 accA = rn_zero16(), accB = rn_zero16();
     DwScale cur = {0.f, 0.f};
     int cur_k = -1;
-    uint64_t cyc[4] = {0, 0, 0, 0};
+    // (ablation build, flag 4096) summed wave cycles: [0] MLP phase, [1]
+    // window staging, [2] walk, [3] chunk tails; inside the MLP phase [4]
+    // model switches (park / unpark / weights), [5] forward recompute, [6]
+    // bwd_window, [7] row stores
+    uint64_t cyc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     float* park = m.park + (size_t)blockIdx.x * K * BWD_WAVES * 2048 + wid * 2048;
     float* rows = m.scratch + (size_t)blockIdx.x * m.rows_cap * MB_ROW;
     const __amdgpu_buffer_rsrc_t rows_rs = rn_rsrc(rows, (uint32_t)m.rows_cap * MB_ROW * 4u);
@@ -1154,12 +1172,13 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         __syncthreads();
 
         // ---- 1. MLP backward per model, rows staged in the block's scratch
-        const bool prof = ABL && (dbg & 4096);
+        const bool prof = ABL && (rn_dbg(dbg) & 4096);
         uint64_t tp0 = prof ? __builtin_amdgcn_s_memtime() : 0;
         for (int kk = 0; kk < K; ++kk) {
             const int k = rev ? K - 1 - kk : kk;
             const int a_k = sCh[2 + k], n_k = sCh[2 + MB_KMAX + k], roff = sCh[2 + 2 * MB_KMAX + k];
             if (n_k == 0) continue;
+            uint64_t ts0 = prof ? __builtin_amdgcn_s_memtime() : 0;
             if (k != cur_k) {
                 __syncthreads();                 // every wave done with sW
                 if (cur_k >= 0) {
@@ -1181,13 +1200,14 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 __syncthreads();
             }
             sw_ok = true;
+            if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[4] += t - ts0; ts0 = t; }
             for (int w0 = 0; w0 < n_k; w0 += BWD_WAVES * 32) {
                 rn_lds_order();
                 const int i = w0 + wid * 32 + c;
                 const bool valid = i < n_k;
                 // ablation 256: every tile reads the chunk's first 32 samples
                 // (cache-resident inputs; timing only)
-                const int64_t s = a_k + (valid ? ((dbg & 256) ? (i & 31) : i) : 0);
+                const int64_t s = a_k + (valid ? ((rn_dbg(dbg) & 256) ? (i & 31) : i) : 0);
                 FwdState st;
                 float ux, uy, uz;
                 // the backward seeds, loaded ahead of the forward recompute
@@ -1200,12 +1220,17 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 tile_forward_rays<CACHE>(a, sT, sW, s, valid,
                                          CACHE == CACHE_READ ? cache_slot(a, s) : nullptr, sRays,
                                          r0, nr_lds, st, ux, uy, uz);
+                if (prof) {
+                    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+                    const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[5] += t - ts0; ts0 = t;
+                }
                 float gscale; bool zero_iter;
                 // ablation 512: no block barriers in the MLP phase (wrong
                 // results; timing of the barrier cost only)
                 const f32x16 dE = bwd_window(a, sW, sImg, sMax, imgY, imgX, st, valid, s, wid,
                                              accA, accB, cur, do_dw, gscale, zero_iter,
-                                             !(dbg & 512), pre);
+                                             !(rn_dbg(dbg) & 512), pre);
+                if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[6] += t - ts0; ts0 = t; }
                 if (valid) {
                     const float ginv = zero_iter ? 0.f : 1.0f / gscale;
                     float* row = rows + (size_t)(roff + i) * MB_ROW;
@@ -1217,6 +1242,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                                            (_Float16)dE[4 * g + 2], (_Float16)dE[4 * g + 3]};
                     if (h == 0) *reinterpret_cast<float4*>(row + 16) = make_float4(ux, uy, uz, ginv);
                 }
+                if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[7] += t - ts0; ts0 = t; }
             }
         }
         if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[0] += t - tp0; tp0 = t; }
@@ -1282,7 +1308,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
             // are identified by their coordinates)
             const bool live_w = __syncthreads_or(nz);
             if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[1] += t - tp0; tp0 = t; }
-            if (live_w && !(dbg & 32)) {
+            if (live_w && !(rn_dbg(dbg) & 32)) {
                 const int ne = max(0, min(MB_WIN, elen_lane - w0));
                 const int n0 = max(0, min(MB_WIN, min(E, n_p) - w0));
                 walk2_window<GM, MB_WIN>(a, sT, wG, wU, ne, n0, grad_rs, G, W, dbg);
@@ -1297,9 +1323,9 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         pgA = W.pgA; pgB = W.pgB; nA = W.nA; nB = W.nB;
         __syncthreads();                         // rings (image region) drained
     }
-    if (ABL && (dbg & 4096) && rn_lane() == 0) {
+    if (ABL && (rn_dbg(dbg) & 4096) && rn_lane() == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
+        for (int q = 0; q < 8; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
     }
     if (GM == 4 && rn_lane() == 0) {             // close this wave's open pages
         if (pgA < G.pool_pages) G.page_meta[pgA] = (uint32_t)wid | (nA << 8);
@@ -1732,11 +1758,13 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 #define FX_ENTRY_BITS 28
 #define FX_DENSE_FIRST_BITS 14
 #define FX_GROWTH_UNITS 268435456.f       // 2^28
-// Binned mode (ctl != NULL, rn_grid_binned_fold): records are int22, summed
-// exactly in int64, so there is no entry cap and no wrap check; the largest
-// record maps to < 2^GB_TARGET_BITS units (8x headroom below the int22 range,
-// like round 2's 2^19 / 2^22), a record at 2^21 units or a pool overflow (the
-// walk ran out of pages) sets the redo flag.
+// Binned mode (ctl != NULL, rn_grid_binned_fold): records are e5m17 (rn_bin.h),
+// summed exactly in int64, so there is no entry cap and no wrap check; the
+// largest record maps to < 2^GB_TARGET_BITS = 2^38 units (256x headroom below
+// 2^46, the first value e5m17 cannot hold: a record that reaches it sets the
+// redo flag -- the bar is exact, every record below it is representable), and
+// so does a pool overflow (the walk ran out of pages) or a fault word the bin
+// pass set (inputs out of range).
 __global__ void __launch_bounds__(64)
 k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
            float* __restrict__ scale_next, FxStats* __restrict__ stats,
@@ -1744,8 +1772,9 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
     const int l = threadIdx.x;
     uint32_t* vmax = stats->vmax;
     const bool binned = ctl != nullptr;
-    bool bad = binned && l == 0 && ctl->pool_next > pool_pages;
-    const float growth = binned ? (float)(GB_V_MAX + 1) : FX_GROWTH_UNITS;
+    // pool overflow, or inputs the bin pass refused (GbCtl::fault)
+    bool bad = binned && l == 0 && (ctl->pool_next > pool_pages || ctl->fault != 0u);
+    const float growth = binned ? GB_GROWTH_UNITS : FX_GROWTH_UNITS;
     if (l < RN_L) {
         // net wrap of an int32 entry: the entries' exact sum differs from the
         // records' exact sum (by a multiple of 2^32)
@@ -2141,7 +2170,7 @@ extern "C" {
 
 void rn_set_debug_flags(int flags) { g_field_dbg = flags; }
 }  // extern "C"
-int rn_debug_flags_internal() { return g_field_dbg; }
+int rn_debug_flags_internal() { return rn_dbg(g_field_dbg); }   // 0 in librn.so
 extern "C" {
 
 int rn_set_level_pairing(uint64_t pairing) {
@@ -2201,7 +2230,7 @@ int rn_field_fwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
-    a.dbg = g_field_dbg;
+    a.dbg = rn_dbg(g_field_dbg);
     dim3 grid(blocks_per_model, n_models);
     if (xyzs) {
         RN_CHECK_ARG(dirs && n_models == 1, "xyz mode needs dirs and a single model");
@@ -2234,7 +2263,7 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
                  extent && frags && dL_dsigma && dL_drgb && grid_grad && dw, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
-    a.dbg = g_field_dbg;
+    a.dbg = rn_dbg(g_field_dbg);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
     a.feat = (rn_half*)feat_cache;
@@ -2322,7 +2351,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  dw && scratch && park, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
-    a.dbg = g_field_dbg;
+    a.dbg = rn_dbg(g_field_dbg);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.dsigma = dL_dsigma; a.drgb = dL_drgb; a.grid_grad = grid_grad; a.dw = dw;
     a.feat = (rn_half*)feat_cache;
@@ -2360,12 +2389,18 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         F.wq = reinterpret_cast<FxStats*>(fx_stats)->wq;
     }
     const dim3 blk(BWD_WAVES * 64);
-    if (fx_mode == 4 && a.dbg) {
-        k_field_bwd_merged<CACHE_READ, true, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
-    } else if (fx_mode == 4) {
+    if constexpr (RN_ABL) {                     // timing studies (librn_abl.so only)
+        if (a.dbg && (fx_mode == 4 || fx_mode == 2 || (fx_mode == 0 && !igrad_lo))) {
+            if (fx_mode == 4) k_field_bwd_merged<CACHE_READ, true, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
+            else if (fx_mode == 2) k_field_bwd_merged<CACHE_READ, true, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
+            else if (feat_cache) k_field_bwd_merged<CACHE_READ, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
+            else k_field_bwd_merged<CACHE_NONE, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
+            RN_CHECK_LAUNCH();
+            return 0;
+        }
+    }
+    if (fx_mode == 4) {
         k_field_bwd_merged<CACHE_READ, false, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
-    } else if (fx_mode == 2 && a.dbg) {
-        k_field_bwd_merged<CACHE_READ, true, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (fx_mode == 2) {
         k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (fx_mode == 3) {
@@ -2373,9 +2408,6 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     } else if (igrad_lo) {
         if (feat_cache) k_field_bwd_merged<CACHE_READ, false, 1><<<blocks, blk, 0, st>>>(a, m, G, F);
         else k_field_bwd_merged<CACHE_NONE, false, 1><<<blocks, blk, 0, st>>>(a, m, G, F);
-    } else if (a.dbg) {
-        if (feat_cache) k_field_bwd_merged<CACHE_READ, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
-        else k_field_bwd_merged<CACHE_NONE, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else {
         if (feat_cache) k_field_bwd_merged<CACHE_READ, false, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
         else k_field_bwd_merged<CACHE_NONE, false, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
@@ -2403,7 +2435,7 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  "merged-order encoding needs mstart, perm and the encoding cache");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
-    a.dbg = g_field_dbg;
+    a.dbg = rn_dbg(g_field_dbg);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
     a.ts = ts; a.ray_of = ray_of; a.rays_o = rays_o; a.rays_d = rays_d;
@@ -2457,7 +2489,7 @@ int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* ray
                  frags && sigma && rgb && mstart && perm && planes && prep, "null pointer");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
-    a.dbg = g_field_dbg;
+    a.dbg = rn_dbg(g_field_dbg);
     a.grid = (const rn_half*)grid_f16; a.frags = (const rn_half*)frags;
     a.sigma = sigma; a.rgb = rgb; a.feat = (rn_half*)feat_cache;
     a.planes = planes; a.plane_stride = plane_stride;

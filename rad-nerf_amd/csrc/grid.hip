@@ -65,9 +65,12 @@ inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
 
 extern "C" {
 
-// 2 (round 4): rn_field_bwd_merged takes the page pool of fx_mode 4 (binned
-// scatter) and its 384-B statistics block is named fx_stats; rn_grid_bin /
-// rn_grid_sum / rn_grid_binned_fold added
+// ABI history: 2 (round 4) rn_field_bwd_merged takes the page pool of
+// fx_mode 4 (binned scatter), its statistics block is named fx_stats;
+// rn_grid_bin / rn_grid_sum / rn_grid_binned_fold added.  3 (round 4) the
+// fx_stats block grew to 640 B (position-weighted sums wq / we).  4 (round 5)
+// binned records are e5m17 (rn_grid_record_encode / _decode), the GbCtl block
+// carries a fault word, rn_grid_bin_layout fills 8 values.
 int rn_version(void) { return RN_ABI_VERSION; }
 
 const char* rn_last_error(void) { return g_err; }

@@ -492,7 +492,7 @@ int rn_ml_march_count(const float* rays_o, const float* rays_d, const float* cen
     RN_CHECK_ARG(rays_o && rays_d && center && half_size && noise && density_bitfields && counts,
                  "null pointer");
     MarchCfg c = make_cfg(cascades, grid_size, max_samples, scale, scale, exp_step_factor);
-    c.abl = (rn_debug_flags_internal() >> 24) & 1;
+    c.abl = rn_dbg(rn_debug_flags_internal() >> 24) & 1;
     if (stage_ts)
         k_ml_march_count<true><<<nblk(n_rays * n_models, 4), 256, 0, (hipStream_t)stream>>>(
             (int)n_rays, n_models, rays_o, rays_d, center, half_size, near_distance, noise,

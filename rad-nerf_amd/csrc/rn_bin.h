@@ -33,26 +33,58 @@ __host__ __device__ __forceinline__ uint32_t gb_slice_bits(uint32_t hsize) {
     return b;
 }
 #define GB_IDX_BITS 20            // entry index within its level
-#define GB_V_BITS 22              // each feature's fixed-point value, two's complement
-#define GB_V_MAX ((1 << (GB_V_BITS - 1)) - 1)
-#define GB_TARGET_BITS 18         // a level's largest record maps to < 2^18 units (8x headroom)
+#define GB_V_BITS 22              // each feature's record value (e5m17, below)
+#define GB_M_BITS 17              // two's-complement mantissa
+#define GB_E_MAX 31               // 5-bit exponent
+#define GB_TARGET_BITS 38         // a level's largest record maps to < 2^38 units (256x headroom)
+#define GB_GROWTH_UNITS 70368744177664.f   // 2^46: a record at or past it is not representable
+
+// A record value x (the gradient times the level's 2^e_l, a float; exact,
+// since 2^e_l is a power of two) is stored as e5m17: m * 2^e with
+//   e = 0,          m = rint(x)            for |x| < 2^15 (exact to one unit),
+//   e = E - 14 > 0, m = rint(x * 2^-e)     for 2^E <= |x| < 2^(E+1), E >= 15,
+// i.e. |m| <= 2^15 with 14 significant bits past the leading one (relative
+// error <= 2^-15 at and above 2^15 units), e <= 31: every |x| < 2^46 is
+// representable.  The unit is 2^-38 of the level's largest record of the
+// previous step, so only gradients below ~2^-39 of it round to zero.
+// Why so fine: with eps = 1e-15, FusedAdam turns any non-zero gradient into an
+// lr-sized step, so an entry flushed to zero changes the update as much as a
+// wrong sign.  Round 4 stored x as a plain int22 (unit 2^-18 of the largest
+// record): at C5's shape 1.3 % of the non-zero entries flushed and 3 Adam
+// steps differed from fp32's by 24 % per level; an e4m18 form (unit 2^-27)
+// still flushed 0.05 % (4.8 %), all of them entries below half a unit
+// (tools/fx_entry_diag.py).  The sum pass adds m << e
+// exactly in int64 (an entry would need 2^25 records at the growth bound to
+// overflow), so the sums stay order-free and bitwise reproducible.
+__host__ __device__ __forceinline__ uint32_t gb_encode(float x) {
+    const uint32_t E = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;   // biased exponent
+    int e = (int)E - (127 + 14);
+    e = e < 0 ? 0 : (e > GB_E_MAX ? GB_E_MAX : e);
+    // clamped before the conversion (|x| >= 2^46 and NaN: the step is redone)
+    const float y = fminf(fmaxf(rintf(ldexpf(x, -e)), -32768.f), 32768.f);
+    return ((uint32_t)(int)y & ((1u << GB_M_BITS) - 1u)) | ((uint32_t)e << GB_M_BITS);
+}
+__host__ __device__ __forceinline__ int64_t gb_decode(uint32_t f) {
+    const int64_t m = (int64_t)((int32_t)(f << (32 - GB_M_BITS)) >> (32 - GB_M_BITS));
+    return m * ((int64_t)1 << ((f >> GB_M_BITS) & (uint32_t)GB_E_MAX));
+}
 
 // Record = u64: [0, 20) entry index within the level, [20, 42) feature 0,
-// [42, 64) feature 1 (int22 fixed point in the level's units 2^e_l).  The
-// level is the page's (a walk page holds one level's records).
-__host__ __device__ __forceinline__ uint64_t gb_pack(uint32_t idx, int32_t q0, int32_t q1) {
+// [42, 64) feature 1 (e5m17 fields in the level's units 2^e_l).  The level is
+// the page's (a walk page holds one level's records).
+__host__ __device__ __forceinline__ uint64_t gb_pack(uint32_t idx, uint32_t f0, uint32_t f1) {
     return (uint64_t)(idx & ((1u << GB_IDX_BITS) - 1u)) |
-           ((uint64_t)((uint32_t)q0 & ((1u << GB_V_BITS) - 1u)) << GB_IDX_BITS) |
-           ((uint64_t)(uint32_t)q1 << (GB_IDX_BITS + GB_V_BITS));
+           ((uint64_t)(f0 & ((1u << GB_V_BITS) - 1u)) << GB_IDX_BITS) |
+           ((uint64_t)(f1 & ((1u << GB_V_BITS) - 1u)) << (GB_IDX_BITS + GB_V_BITS));
 }
 __host__ __device__ __forceinline__ uint32_t gb_idx(uint64_t r) {
     return (uint32_t)r & ((1u << GB_IDX_BITS) - 1u);
 }
 __host__ __device__ __forceinline__ int64_t gb_v0(uint64_t r) {
-    return (int64_t)(r << (64 - GB_IDX_BITS - GB_V_BITS)) >> (64 - GB_V_BITS);
+    return gb_decode((uint32_t)(r >> GB_IDX_BITS) & ((1u << GB_V_BITS) - 1u));
 }
 __host__ __device__ __forceinline__ int64_t gb_v1(uint64_t r) {
-    return (int64_t)r >> (GB_IDX_BITS + GB_V_BITS);
+    return gb_decode((uint32_t)(r >> (GB_IDX_BITS + GB_V_BITS)));
 }
 
 int rn_debug_flags_internal();    // rn_set_debug_flags (field.hip), host side
@@ -65,8 +97,18 @@ int rn_fx_check_binned(const float* fx_scale_cur, float* fx_scale_next, uint32_t
 struct GbCtl {
     uint32_t pool_next;           // pages taken by the walk (may exceed the pool: overflow)
     uint32_t level_npages[16];    // pages of each level (the bin pass fills level_pages)
-    uint32_t pad[15];
+    uint32_t fault;               // GB_FAULT_* bits: inputs the passes refused (-> redo)
+    uint32_t pad[14];
 };
+// fault bits: a page's meta names a level >= 16 or more than GB_PAGE records
+// (bin pass); a record's entry index lies outside its level (bin pass); a
+// level's page list overflowed the pool (bin pass); a page id or run outside
+// the pool / page (sum pass).  The bin pass's faults set the redo flag
+// (k_fx_check runs between the bin and sum passes); the sum pass only skips.
+#define GB_FAULT_META 1u
+#define GB_FAULT_INDEX 2u
+#define GB_FAULT_LIST 4u
+#define GB_FAULT_RUN 8u
 
 // Pool: page_meta[p] = level | count << 8 (written when the page closes);
 // pages_in [pool][GB_PAGE] u64 (walk order), pages_out (slice order),
@@ -81,4 +123,5 @@ struct GbPool {
     uint32_t* level_pages;
     uint32_t pool_pages;
     uint8_t slice_bits[16];       // gb_slice_bits of each level's size
+    uint32_t hsize[16];           // entries of each level (the bin pass checks indices)
 };

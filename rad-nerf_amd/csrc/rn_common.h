@@ -17,6 +17,19 @@
 #define RN_SQRT3 1.73205080757f
 #define RN_WAVE 64
 
+// Timing studies (tools/ablate.py, bin_probe.py, march_probe.py) switch parts
+// of kernels off or swap in variants through rn_set_debug_flags.  Only the
+// ablation build reads those switches: librn_abl.so (-DRN_ABLATION, tools
+// only).  In librn.so RN_ABL is 0, rn_dbg() folds every switch to 0 at compile
+// time, the variant kernels are not instantiated, and each kernel has exactly
+// one code path.
+#ifdef RN_ABLATION
+#define RN_ABL 1
+#else
+#define RN_ABL 0
+#endif
+__host__ __device__ constexpr int rn_dbg(int flags) { return RN_ABL ? flags : 0; }
+
 // ---------------------------------------------------------------------------
 // status / error plumbing shared by every C-ABI entry point
 // ---------------------------------------------------------------------------

@@ -63,7 +63,7 @@ __device__ __forceinline__ void load_sample(const FieldArgs& a, int64_t s, float
         dx = a.dirs[3 * s]; dy = a.dirs[3 * s + 1]; dz = a.dirs[3 * s + 2];
     } else {
         // ablation 8192 (timing only): no dependent ray lookup
-        const int r = (a.dbg & 8192) ? 0 : a.ray_of[s];
+        const int r = (rn_dbg(a.dbg) & 8192) ? 0 : a.ray_of[s];
         const float t = a.ts[s];
         dx = a.rays_d[3 * r]; dy = a.rays_d[3 * r + 1]; dz = a.rays_d[3 * r + 2];
         // bit-identical to the march's sample position (march.hip march_step)
@@ -175,7 +175,7 @@ __device__ __forceinline__ void encode_lane(const FieldArgs& a, const LvTab& T,
                                             __amdgpu_buffer_rsrc_t rs, int h, float ux, float uy,
                                             float uz, bool valid, half8& e0, half8& e1) {
     float f[16];
-    const bool load = valid && !(a.dbg & 128);
+    const bool load = valid && !(rn_dbg(a.dbg) & 128);
 #pragma unroll
     for (int lb = 0; lb < RN_L; lb += 4) {
         // per level: the cell's x, the weights' fractions, and the x-free part
@@ -331,7 +331,7 @@ __device__ __forceinline__ uint32_t encode_tiles(const FieldArgs& a, __amdgpu_bu
 #pragma unroll
         for (int r = 0; r < 4; ++r) xch(rw[r], ROW[0][r], ROW[1][r]);
     }
-    const bool noload = a.dbg & 128;
+    const bool noload = rn_dbg(a.dbg) & 128;
     uint32_t off[8];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -550,12 +550,12 @@ __device__ __forceinline__ void tile_forward_pos(const FieldArgs& a, const LvTab
             st.e1 = __builtin_nontemporal_load(fc + 1);
         }
     } else {
-        if (a.dbg & 256) { st.e0 = rn_zero8(); st.e1 = rn_zero8(); asm volatile("" :: "v"(ux), "v"(uy), "v"(uz)); }
+        if (rn_dbg(a.dbg) & 256) { st.e0 = rn_zero8(); st.e1 = rn_zero8(); asm volatile("" :: "v"(ux), "v"(uy), "v"(uz)); }
         else encode_lane(a, T, rn_rsrc(a.grid, a.grid_bytes), h, ux, uy, uz, valid, st.e0, st.e1);
         if (CACHE == CACHE_WRITE && valid) { fc[0] = st.e0; fc[1] = st.e1; }
     }
     st.sh = sh_lane(dx, dy, dz, h);
-    if (a.dbg & 4096) {                 // ablation: no MLP (outputs are garbage)
+    if (rn_dbg(a.dbg) & 4096) {                 // ablation: no MLP (outputs are garbage)
         st.out = rn_zero16(); st.g0 = 0.f;
         asm volatile("" :: "v"(st.e0), "v"(st.e1), "v"(st.sh));
     } else {

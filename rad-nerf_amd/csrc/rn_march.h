@@ -172,7 +172,7 @@ __device__ int march_ray_wave(float ox, float oy, float oz, float dx, float dy, 
 #pragma unroll 16
                 for (int i = 0; i < RN_WAVE - 1; ++i) { const float nt = t + d0; t = i < lane ? nt : t; }
             }
-        } else if (c.abl & 1) {          // timing only: the chain's cost
+        } else if (rn_dbg(c.abl) & 1) {  // timing only: the chain's cost
             t = fmaf((float)lane, rn_calc_dt(tb, c.esf, c.max_samples, c.grid_size, c.dt_scale), tb);
         } else {
 #pragma unroll 8

@@ -148,7 +148,7 @@ __device__ __forceinline__ void rn_dw_tile(const rn_half* img_y, int ya, const r
     f32x16 acc = rn_zero16();
     acc = rn_mfma(rn_img_read(img_y, ya, 0), rn_img_read(img_x, xa, 0), acc);
     acc = rn_mfma(rn_img_read(img_y, ya, 1), rn_img_read(img_x, xa, 1), acc);
-    if (dbg & 8) { asm volatile("" :: "v"(acc)); return; }
+    if (rn_dbg(dbg) & 8) { asm volatile("" :: "v"(acc)); return; }
     const int lane = rn_lane(), col = lane & 31, h = lane >> 5;
     float* base = dw_lds + off + in_base + col;
 #pragma unroll

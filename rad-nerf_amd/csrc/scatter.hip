@@ -53,7 +53,12 @@ k_grid_bin(GbPool P, bool rotate) {
     if (PF && blockIdx.x < np) load_page(blockIdx.x, r, GB_PAGE);
     for (uint32_t p = blockIdx.x; p < np; p += gridDim.x) {
         const uint32_t meta = P.page_meta[p];
-        const uint32_t l = meta & 31u, n = meta >> 8;
+        uint32_t l = meta & 0xffu, n = meta >> 8;
+        if (l >= RN_L || n > GB_PAGE) {                 // a corrupt meta: refuse the page
+            if (tid == 0) atomicOr(&P.ctl->fault, GB_FAULT_META);
+            l = 0u; n = 0u;
+        }
+        const uint32_t hs = P.hsize[l];
         for (int i = tid; i < GB_MAX_BINS; i += THREADS) sHist[i] = 0u;
         __syncthreads();
         if (!PF) load_page(p, r, n);
@@ -61,14 +66,25 @@ k_grid_bin(GbPool P, bool rotate) {
         if (PF && p + gridDim.x < np) load_page(p + gridDim.x, rn, GB_PAGE);
         uint32_t key[PT];
         const uint32_t sb = P.slice_bits[l];
+        bool bad_idx = false;
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
             const uint32_t i = tid + THREADS * j;
+            key[j] = ~0u;
             if (i < n) {
-                const uint32_t b = gb_idx(r[j]) >> sb;
-                key[j] = (b << 16) | atomicAdd(&sHist[b], 1u);
+                const uint32_t e = gb_idx(r[j]);
+                // an index outside the level would bin past its slices (and
+                // past sHist): refused, and the step is redone
+                if (e < hs) {
+                    const uint32_t b = e >> sb;
+                    key[j] = (b << 16) | atomicAdd(&sHist[b], 1u);
+                } else {
+                    bad_idx = true;
+                }
             }
         }
+        if (__builtin_amdgcn_ballot_w64(bad_idx) != 0ull && lane == 0)
+            atomicOr(&P.ctl->fault, GB_FAULT_INDEX);
         __syncthreads();
         if (wid == 0) {
             // exclusive scan of the bins, GB_BPL per lane, in an order rotated
@@ -101,14 +117,15 @@ k_grid_bin(GbPool P, bool rotate) {
             }
             if (lane == 0 && n > 0) {
                 const uint32_t slot = atomicAdd(&P.ctl->level_npages[l], 1u);
-                P.level_pages[(size_t)l * P.pool_pages + slot] = p;
+                if (slot < P.pool_pages) P.level_pages[(size_t)l * P.pool_pages + slot] = p;
+                else atomicOr(&P.ctl->fault, GB_FAULT_LIST);     // a control block not reset
             }
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < PT; ++j) {
             const uint32_t i = tid + THREADS * j;
-            if (i < n) sRec[sHist[key[j] >> 16] + (key[j] & 0xffffu)] = r[j];
+            if (i < n && key[j] != ~0u) sRec[sHist[key[j] >> 16] + (key[j] & 0xffffu)] = r[j];
         }
         __syncthreads();
         uint64_t* dst = P.pages_out + (size_t)p * GB_PAGE;
@@ -255,7 +272,14 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
                 i += start;
                 i = i >= npg ? i - npg : i;
                 pg = lp[i];
-                d = P.desc[(size_t)pg * GB_MAX_BINS + b];
+                // a page id outside the pool or a run past its page (the bin
+                // pass writes neither): skipped, and the fault word says so
+                const bool pg_ok = pg < P.pool_pages;
+                d = pg_ok ? P.desc[(size_t)pg * GB_MAX_BINS + b] : 0u;
+                if (!pg_ok || (d & 0xffffu) + (d >> 16) > GB_PAGE) {
+                    atomicOr(&P.ctl->fault, GB_FAULT_RUN);
+                    pg = 0u; d = 0u;
+                }
             }
         };
         uint32_t g = grab(), pg, d;
@@ -315,6 +339,7 @@ int rn_grid_bin_layout(int32_t* out) {
     RN_CHECK_ARG(out, "null pointer");
     out[0] = GB_PAGE; out[1] = GB_MAX_BINS; out[2] = (int32_t)GB_SLICE;
     out[3] = (int32_t)sizeof(GbCtl); out[4] = GB_IDX_BITS; out[5] = GB_V_BITS;
+    out[6] = GB_M_BITS; out[7] = GB_TARGET_BITS;
     return 0;
 }
 
@@ -325,6 +350,20 @@ int rn_grid_slice_bits(const uint32_t* level_hsize, int32_t* out) {
                      "level too large for binning");
         out[l] = (int32_t)gb_slice_bits(level_hsize[l]);
     }
+    return 0;
+}
+
+int rn_grid_record_encode(const float* x, int64_t n, uint32_t* out) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    RN_CHECK_ARG(n == 0 || (x && out), "null pointer");
+    for (int64_t i = 0; i < n; ++i) out[i] = gb_encode(x[i]);
+    return 0;
+}
+
+int rn_grid_record_decode(const uint32_t* f, int64_t n, int64_t* out) {
+    RN_CHECK_ARG(n >= 0, "bad size");
+    RN_CHECK_ARG(n == 0 || (f && out), "null pointer");
+    for (int64_t i = 0; i < n; ++i) out[i] = gb_decode(f[i]);
     return 0;
 }
 
@@ -339,6 +378,7 @@ int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_met
         RN_CHECK_ARG(level_hsize[l] >= 1 && level_hsize[l] <= (GB_MAX_BINS << GB_SLICE_BITS) &&
                          level_hsize[l] <= (1u << GB_IDX_BITS), "level too large for binning");
         P.slice_bits[l] = (uint8_t)gb_slice_bits(level_hsize[l]);
+        P.hsize[l] = level_hsize[l];
     }
     P.ctl = (GbCtl*)ctl; P.page_meta = (uint32_t*)page_meta; P.pages_in = (uint64_t*)pages_in;
     P.pages_out = pages_out; P.desc = desc; P.level_pages = level_pages;
@@ -346,13 +386,17 @@ int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_met
     // (timing studies only: bit 20 no per-page rotation of the run layout;
     // bits 22-23 the variant: 1 = 512 threads with the next page prefetched,
     // 2 = 256 threads)
-    const int dbg = rn_debug_flags_internal();
+    const int dbg = rn_debug_flags_internal();       // 0 in librn.so
     const bool rotate = !((dbg >> 20) & 1);
     const int var = (dbg >> 22) & 3;
     hipStream_t st = (hipStream_t)stream;
-    if (var == 1) k_grid_bin<512, true><<<blocks, 512, 0, st>>>(P, rotate);
-    else if (var == 2) k_grid_bin<256, false><<<blocks, 256, 0, st>>>(P, rotate);
-    else k_grid_bin<1024, false><<<blocks, 1024, 0, st>>>(P, rotate);
+    bool done = false;
+    if constexpr (RN_ABL) {
+        done = var == 1 || var == 2;
+        if (var == 1) k_grid_bin<512, true><<<blocks, 512, 0, st>>>(P, rotate);
+        else if (var == 2) k_grid_bin<256, false><<<blocks, 256, 0, st>>>(P, rotate);
+    }
+    if (!done) k_grid_bin<1024, false><<<blocks, 1024, 0, st>>>(P, rotate);
     RN_CHECK_LAUNCH();
     return 0;
 }
@@ -360,10 +404,12 @@ int rn_grid_bin(const uint32_t* level_hsize, void* ctl, const uint32_t* page_met
 int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const void* ctl,
                 const uint32_t* desc, const uint32_t* level_pages, const uint64_t* pages_out,
                 int32_t pool_pages, const float* fx_scale, const int32_t* redo, float* grid_grad,
-                void* stream) {
+                int32_t level_lo, int32_t level_hi, void* stream) {
     RN_CHECK_ARG(level_offset && level_hsize && ctl && desc && level_pages && pages_out &&
                  fx_scale && grid_grad, "null pointer");
     RN_CHECK_ARG(pool_pages >= 1, "bad sizes");
+    RN_CHECK_ARG(level_lo >= 0 && level_lo <= level_hi && level_hi <= RN_L,
+                 "levels: 0 <= level_lo <= level_hi <= 16");
     GbSumArgs s{};
     uint32_t total = 0;
     for (int q = 0; q < RN_L; ++q) {            // the finest (heaviest) levels first
@@ -372,9 +418,12 @@ int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const
                          level_hsize[l] <= (1u << GB_IDX_BITS), "level too large for binning");
         s.first[q] = total;
         const uint32_t sb = gb_slice_bits(level_hsize[l]);
-        total += (level_hsize[l] + (1u << sb) - 1) >> sb;
+        // levels outside [level_lo, level_hi) get no workgroups (an empty
+        // range of blockIdx: the kernel's level search never lands on them)
+        if (l >= level_lo && l < level_hi) total += (level_hsize[l] + (1u << sb) - 1) >> sb;
     }
     s.first[RN_L] = total;
+    if (total == 0) return 0;
     for (int l = 0; l < RN_L; ++l) { s.off[l] = level_offset[l]; s.hs[l] = level_hsize[l]; }
     GbPool P{};
     P.ctl = (GbCtl*)ctl; P.desc = (uint32_t*)desc; P.level_pages = (uint32_t*)level_pages;
@@ -382,23 +431,41 @@ int rn_grid_sum(const uint32_t* level_offset, const uint32_t* level_hsize, const
     for (int l = 0; l < RN_L; ++l) P.slice_bits[l] = (uint8_t)gb_slice_bits(level_hsize[l]);
     const size_t lds = (size_t)GB_SLICE * 2 * sizeof(int64_t) + 16;   // + the group counter
     // ablations (timing studies only): bit 16 no LDS adds, bit 21 per-phase cycles
-    const int dbg = rn_debug_flags_internal() >> 16;
+    const int dbg = rn_debug_flags_internal() >> 16;   // 0 in librn.so
     hipStream_t st = (hipStream_t)stream;
-#define GB_SUM_LAUNCH(A, PR) \
-    k_grid_sum<A, PR><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad)
-    if (dbg & 32) GB_SUM_LAUNCH(0, true);
-    else if ((dbg & 1) && (dbg & 0x1c)) {        // bits 18-20 with 16: bisection (timing)
-        const int bis = (dbg >> 2) & 7;
-        if (bis == 1) k_grid_sum<1, false, 1><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
-        else if (bis == 2) k_grid_sum<1, false, 2><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
-        else if (bis == 3) k_grid_sum<1, false, 3><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
-        else k_grid_sum<0, false, 4><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad);
+#define GB_SUM_LAUNCH(A, PR, BI) \
+    k_grid_sum<A, PR, BI><<<total, GB_SUM_THREADS, lds, st>>>(P, s, fx_scale, redo, grid_grad)
+    bool done = false;
+    if constexpr (RN_ABL) {
+        done = true;
+        if (dbg & 32) GB_SUM_LAUNCH(0, true, 0);
+        else if ((dbg & 1) && (dbg & 0x1c)) {    // bits 18-20 with 16: bisection (timing)
+            const int bis = (dbg >> 2) & 7;
+            if (bis == 1) GB_SUM_LAUNCH(1, false, 1);
+            else if (bis == 2) GB_SUM_LAUNCH(1, false, 2);
+            else if (bis == 3) GB_SUM_LAUNCH(1, false, 3);
+            else GB_SUM_LAUNCH(0, false, 4);
+        }
+        else if (dbg & 1) GB_SUM_LAUNCH(1, false, 0);
+        else done = false;
     }
-    else if (dbg & 1) GB_SUM_LAUNCH(1, false);
-    else GB_SUM_LAUNCH(0, false);
+    if (!done) GB_SUM_LAUNCH(0, false, 0);
 #undef GB_SUM_LAUNCH
     RN_CHECK_LAUNCH();
     return 0;
+}
+
+int rn_grid_bin_check(const uint32_t* level_hsize, void* ctl, const uint32_t* page_meta,
+                      const uint64_t* pages_in, uint64_t* pages_out, uint32_t* desc,
+                      uint32_t* level_pages, int32_t pool_pages, const float* fx_scale_cur,
+                      float* fx_scale_next, uint32_t* fx_stats, int32_t* fx_redo, void* stream) {
+    RN_CHECK_ARG(fx_scale_cur && fx_scale_next && fx_stats && fx_redo, "null pointer");
+    RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
+    int st = rn_grid_bin(level_hsize, ctl, page_meta, pages_in, pages_out, desc, level_pages, pool_pages,
+                         2048, stream);
+    if (st) return st;
+    return rn_fx_check_binned(fx_scale_cur, fx_scale_next, fx_stats, fx_redo, ctl,
+                              (uint32_t)pool_pages, stream);
 }
 
 int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsize, void* ctl,
@@ -406,16 +473,12 @@ int rn_grid_binned_fold(const uint32_t* level_offset, const uint32_t* level_hsiz
                         uint32_t* desc, uint32_t* level_pages, int32_t pool_pages,
                         const float* fx_scale_cur, float* fx_scale_next, uint32_t* fx_stats,
                         int32_t* fx_redo, float* grid_grad, void* stream) {
-    RN_CHECK_ARG(fx_scale_cur && fx_scale_next && fx_stats && fx_redo, "null pointer");
-    RN_CHECK_ARG(fx_scale_cur != fx_scale_next, "scale_cur and scale_next must differ");
-    int st = rn_grid_bin(level_hsize, ctl, page_meta, pages_in, pages_out, desc, level_pages, pool_pages,
-                         2048, stream);
-    if (st) return st;
-    st = rn_fx_check_binned(fx_scale_cur, fx_scale_next, fx_stats, fx_redo, ctl,
-                            (uint32_t)pool_pages, stream);
+    const int st = rn_grid_bin_check(level_hsize, ctl, page_meta, pages_in, pages_out, desc,
+                                     level_pages, pool_pages, fx_scale_cur, fx_scale_next, fx_stats,
+                                     fx_redo, stream);
     if (st) return st;
     return rn_grid_sum(level_offset, level_hsize, ctl, desc, level_pages, pages_out, pool_pages,
-                       fx_scale_cur, fx_redo, grid_grad, stream);
+                       fx_scale_cur, fx_redo, grid_grad, 0, RN_L, stream);
 }
 
 }  // extern "C"

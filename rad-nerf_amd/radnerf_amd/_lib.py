@@ -11,6 +11,11 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RADNERF_LIB", os.path.join(_HERE, "librn.so"))
+# timing studies only (tools/ablate.py, bin_probe.py, march_probe.py): the same
+# sources built with -DRN_ABLATION, where rn_set_debug_flags switches kernel
+# parts off and selects variant kernels (csrc/rn_common.h RN_ABL).  librn.so
+# ignores the switches and holds one code path per kernel.
+ABLATION_LIB_PATH = os.path.join(_HERE, "librn_abl.so")
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -62,8 +67,11 @@ SIGNATURES = {
     "rn_grid_bin_layout": [P],
     "rn_debug_gb_cycles": [P],
     "rn_grid_slice_bits": [P, P],
+    "rn_grid_record_encode": [P, I64, P],
+    "rn_grid_record_decode": [P, I64, P],
     "rn_grid_bin": [P, P, P, P, P, P, P, I32, I32, P],
-    "rn_grid_sum": [P, P, P, P, P, P, I32, P, P, P, P],
+    "rn_grid_sum": [P, P, P, P, P, P, I32, P, P, P, I32, I32, P],
+    "rn_grid_bin_check": [P, P, P, P, P, P, P, I32, P, P, P, P, P],
     "rn_grid_binned_fold": [P, P, P, P, P, P, P, P, I32, P, P, P, P, P, P],
     "rn_render_test": [P, P, P, I64, I32, P, I64, I32, F32, F32, I32, I32, P, P, P, P, P, P, P,
                        P, F32, P, P, P, P, I32, P],
@@ -86,7 +94,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 _lib = None
 
 
@@ -130,10 +138,11 @@ class _Lib:
     def bin_layout(self):
         """the binned scatter's page layout (csrc/rn_bin.h, rn_grid_bin_layout)"""
         if getattr(self, "_bin_layout", None) is None:
-            out = (ctypes.c_int32 * 6)()
+            out = (ctypes.c_int32 * 8)()
             self.grid_bin_layout(out)
             self._bin_layout = dict(page=out[0], bins=out[1], slice=out[2], ctl_bytes=out[3],
-                                    idx_bits=out[4], v_bits=out[5])
+                                    idx_bits=out[4], v_bits=out[5], m_bits=out[6],
+                                    target_bits=out[7])
         return self._bin_layout
 
     def check_version(self):
@@ -151,6 +160,16 @@ def lib():
         _lib = _Lib(LIB_PATH)
         _lib.check_version()
     return _lib
+
+
+def use_ablation_build():
+    """Timing-study tools: load librn_abl.so instead of librn.so.  Call before
+    the first lib() of the process (the product path never calls it)."""
+    global LIB_PATH
+    if _lib is not None and _lib.path != ABLATION_LIB_PATH:
+        raise RuntimeError("librn.so is already loaded in this process")
+    LIB_PATH = ABLATION_LIB_PATH
+    return lib()
 
 
 def exported_symbols():

@@ -250,6 +250,23 @@ class GradAllReduce:
         return self.views
 
 
+def step_ranges(ar, level_offset, split_level):
+    """The data-parallel step's collective schedule over a GradAllReduce of
+    [grid, MLP, gate] (bench.py's headline step, N > 1), as [a, b) ranges of
+    the flat buffer in launch order:
+      "rest"   MLP + gate gradients, once field_bwd has written them;
+      "fine"   the hash grid's levels [split_level, 16) -- the tail of the
+               level-major table, the fine hashed levels -- once the fold has
+               summed them (FusedMLRenderer.after_grid_levels), so their
+               collective overlaps the coarse levels' sum pass;
+      "coarse" levels [0, split_level) after the fold.
+    split_level 0: "fine" is the whole grid and "coarse" empty.  The three
+    ranges tile the flat buffer (tests/test_dist.py)."""
+    g0, g1 = ar.param_range(0, 1)
+    cut = g0 + 2 * int(level_offset[split_level]) if 0 < split_level < 16 else g0
+    return {"rest": ar.param_range(1), "fine": (cut, g1), "coarse": (g0, cut)}
+
+
 def broadcast_buffers(module, src=0):
     """Keep density grids / bitfields identical across ranks."""
     if dist.is_initialized() and dist.get_world_size() > 1:

@@ -115,9 +115,9 @@ class Workspace:
         """Page pool of the binned grid-gradient scatter (fx_mode 4,
         rn_grid_binned_fold; csrc/rn_bin.h): control block, page levels /
         fills, the pages (u64 records; the bin pass sorts each page in place),
-        per-page slice runs, per-level page lists, and a pinned word that
-        receives the pages the last backward took (read without a sync: the
-        pool grows for later steps; a step that overflows is redone in fp32)."""
+        per-page slice runs, per-level page lists (a step that overflows the
+        pool is redone in fp32; _bin_pool grows it from the counts the
+        backwards read back)."""
         b = getattr(self, "_bin", None)
         if b is None or b["pages"] < pages:
             lay = lib().bin_layout()
@@ -128,9 +128,7 @@ class Workspace:
                 meta=torch.zeros(pages, **i),
                 recs=torch.empty(pages * lay["page"], device=self.device, dtype=torch.int64),
                 desc=torch.empty(pages * lay["bins"], **i),
-                lpages=torch.empty(16 * pages, **i),
-                seen=torch.zeros(1, dtype=torch.int32, pin_memory=True),
-                seen_ev=None)
+                lpages=torch.empty(16 * pages, **i))
         return b
 
     def bwd_scratch(self, blocks, max_chunk, max_samples=MAX_SAMPLES):
@@ -272,6 +270,15 @@ class FusedMLRenderer:
         # called right after the merged field_bwd launch (stream order), when
         # the MLP gradient is final (data-parallel early all-reduce)
         self.after_field_bwd = None
+        # called (stream order) when the grid gradient of levels
+        # [grid_split_level, 16) -- the tail of the flat table, the fine hashed
+        # levels -- is final, with grid_split_level as argument; the binned
+        # fold then sums levels [0, grid_split_level), so a data-parallel
+        # caller's collective of the fine levels overlaps it.  With the int32
+        # fold (one short pass over every level) it is called with 0 after the
+        # fold and the redo launch, when the whole table is final.
+        self.after_grid_levels = None
+        self.grid_split_level = 8
         # record HIP events around every launch (True) or the named ones (a set)
         self.trace = False
         self.events = {}
@@ -286,6 +293,20 @@ class FusedMLRenderer:
         L_call(*args)
         b.record(stream)
         self.events.setdefault(name, []).append((a, b))
+
+    def _ev_open(self, name):
+        """start one event span over several launches (closed by _ev_close)"""
+        if not self.trace or (self.trace is not True and name not in self.trace):
+            return None
+        a = torch.cuda.Event(enable_timing=True)
+        a.record()
+        return (name, a)
+
+    def _ev_close(self, span):
+        if span is not None:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record()
+            self.events.setdefault(span[0], []).append((span[1], b))
 
     def _side(self, dev):
         """Side stream for the gate MLP: it runs beside the march (forward) and
@@ -470,26 +491,9 @@ class FusedMLRenderer:
                 # after the fold / bin + sum below: a data-parallel caller
                 # starts the MLP / gate all-reduce now (bench.py)
                 self.after_field_bwd()
-            if use_bin:
-                # bin + sum the pages into grid_grad (or flag the step for the
-                # fp32 redo: a record past the int22 range, a pool overflow)
-                self._ev("fx_fold", L.grid_binned_fold, lo, lh, pool["ctl"].data_ptr(),
-                         pool["meta"].data_ptr(), pool["recs"].data_ptr(),
-                         pool["recs"].data_ptr(), pool["desc"].data_ptr(),
-                         pool["lpages"].data_ptr(), pool["pages"], cur.data_ptr(),
-                         nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(),
-                         grid_grad.data_ptr(), st)
-                pool["seen"].copy_(pool["ctl"][:1], non_blocking=True)
-                pool["seen_ev"] = torch.cuda.Event()
-                pool["seen_ev"].record(torch.cuda.current_stream(grid_grad.device))
-            elif use_fx:
-                # fold the fixed-point sums into grid_grad (or flag the step for
-                # the fp32 redo), next step's scales; the redo launch exits at
-                # once unless flagged (no host synchronisation either way)
-                self._ev("fx_fold", L.grid_fx_fold, lo, lh, lr, acc.data_ptr(), cur.data_ptr(),
-                         nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(),
-                         st)
-            if use_fx:
+            def fx_redo():
+                # the fp32 redo of a flagged step's grid scatter: exits at once
+                # unless the fold / check set the flag (no host synchronisation)
                 self._ev("fx_redo", L.field_bwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                          rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                          w.seg_count.data_ptr(), w.mstart.data_ptr(),
@@ -499,7 +503,52 @@ class FusedMLRenderer:
                          scratch.data_ptr(), rows, park.data_ptr(), self.max_chunk,
                          self.merged_blocks, None, None, None, None, cur.data_ptr(), None,
                          redo.data_ptr(), 3, None, None, None, 0, st)
+
+            if use_bin:
+                # bin the pages and check the step (a record past e5m17's
+                # range, a pool overflow or a refused input flags it for the
+                # fp32 redo), run the redo launch (the sums exit when flagged,
+                # so it can go first), then sum the fine levels, hand them to
+                # after_grid_levels (their all-reduce overlaps the rest) and sum
+                # the coarse levels
+                span = self._ev_open("fx_bin")
+                L.grid_bin_check(lh, pool["ctl"].data_ptr(), pool["meta"].data_ptr(),
+                                 pool["recs"].data_ptr(), pool["recs"].data_ptr(),
+                                 pool["desc"].data_ptr(), pool["lpages"].data_ptr(), pool["pages"],
+                                 cur.data_ptr(), nxt.data_ptr(), stats.data_ptr(),
+                                 redo.data_ptr(), st)
+                # the pages this backward took, read back without a sync
+                # (_bin_pool reads it BIN_LAG backwards later)
+                seen = self._bin_seen(w)
+                seen[0].copy_(pool["ctl"][:1], non_blocking=True)
+                seen[1].record(torch.cuda.current_stream(grid_grad.device))
+                self._ev_close(span)
+                fx_redo()
+                span = self._ev_open("fx_sum")
+                split = max(0, min(16, int(self.grid_split_level))) if self.after_grid_levels else 0
+                sums = ((split, 16), (0, split)) if split > 0 else ((0, 16),)
+                for i, (l0, l1) in enumerate(sums):
+                    L.grid_sum(lo, lh, pool["ctl"].data_ptr(), pool["desc"].data_ptr(),
+                               pool["lpages"].data_ptr(), pool["recs"].data_ptr(), pool["pages"],
+                               cur.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(), l0, l1, st)
+                    if i == 0 and split > 0:
+                        self.after_grid_levels(split)
+                self._ev_close(span)
+                if split == 0 and self.after_grid_levels is not None:
+                    self.after_grid_levels(0)
                 w.fx_i ^= 1
+            elif use_fx:
+                # fold the fixed-point sums into grid_grad (or flag the step for
+                # the fp32 redo), next step's scales; then the redo launch
+                self._ev("fx_fold", L.grid_fx_fold, lo, lh, lr, acc.data_ptr(), cur.data_ptr(),
+                         nxt.data_ptr(), stats.data_ptr(), redo.data_ptr(), grid_grad.data_ptr(),
+                         st)
+                fx_redo()
+                if self.after_grid_levels is not None:
+                    self.after_grid_levels(0)
+                w.fx_i ^= 1
+            elif self.after_grid_levels is not None:
+                self.after_grid_levels(0)             # fp32 atomics: final after field_bwd
             if self.int_grad:
                 self._ev("igrad_to_f32", L.igrad_to_f32, grid_grad.numel(), ig[0], ig[1], ig[2],
                          grid_grad.data_ptr(), st)
@@ -508,9 +557,31 @@ class FusedMLRenderer:
                      w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),
                      w.feat.data_ptr() if self.feat_cache else None, self.bwd_blocks, st)
 
+    # pool growth reads the page count of the binned backward this many
+    # backwards back, waiting for it if needed (reading whichever
+    # count had arrived made the pool size -- and so which steps after an
+    # overflow were binned and which redone in fp32 -- depend on host timing)
+    BIN_LAG = 2
+
+    def _bin_seen(self, w):
+        """the next of BIN_LAG + 1 pinned (count, event) slots, in turn"""
+        ring = getattr(w, "_bin_ring", None)
+        if ring is None:
+            ring = w._bin_ring = [[torch.zeros(1, dtype=torch.int32, pin_memory=True), None,
+                                   -1] for _ in range(self.BIN_LAG + 1)]
+            w._bin_n = 0
+        slot = ring[w._bin_n % len(ring)]
+        slot[1] = torch.cuda.Event()
+        slot[2] = w._bin_n
+        w._bin_n += 1
+        return slot
+
     def _bin_pool(self, w):
-        """The page pool for this backward, grown when the last binned
-        backward's page count (read back without a sync) came near its size."""
+        """The page pool for this backward: sized from the records per (ray,
+        sub-NeRF) at first, then grown when the binned backward BIN_LAG
+        backwards back took more than 7/8 of it (its count, read back
+        asynchronously, is waited for here: a function of the step sequence,
+        not of how far the host runs ahead)."""
         lay = lib().bin_layout()
         b = getattr(w, "_bin", None)
         if b is None:
@@ -520,11 +591,15 @@ class FusedMLRenderer:
                     2 * 8 * self.merged_blocks)
         else:
             need = b["pages"]
-            ev = b["seen_ev"]
-            if ev is not None and ev.query():
-                used = int(b["seen"][0])
-                if used * 8 > need * 7:          # above 7/8: grow to 1.5x what was used
-                    need = used * 3 // 2 + 64
+            ring = getattr(w, "_bin_ring", None)
+            n = getattr(w, "_bin_n", 0) - self.BIN_LAG
+            if ring is not None and n >= 0:
+                slot = ring[n % len(ring)]
+                if slot[2] == n and slot[1] is not None:
+                    slot[1].synchronize()
+                    used = int(slot[0][0])
+                    if used * 8 > need * 7:      # above 7/8: grow to 1.5x what was used
+                        need = used * 3 // 2 + 64
         return w.bin_pool(need)
 
     # ----------------------------------------------------------------- backward

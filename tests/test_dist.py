@@ -156,10 +156,17 @@ def test_bench_self_launch_gloo():
     # the N > 1 collective fields: the early MLP + gate
     # bucket and 4 grid buckets, timed, with the bytes each rank moves
     c = rec["comm"]
-    assert c["mean_ok"] and c["buckets_per_step"] == 5 and c["allreduce_ms"] > 0
+    # MLP + gate, the fine grid levels in 4 buckets, the coarse levels (VERDICT
+    # r04 item 6): the same mean as one plain all-reduce, bit for bit
+    assert c["mean_ok"] and c["buckets_per_step"] == 6 and c["allreduce_ms"] > 0
+    rg = c["ranges"]
     from radnerf_amd import layout as LY
     n = (2 * int(LY.grid_levels(0.5)["n_entries"]) + 2 * LY.FIELD_PARAMS + LY.gate_params(2)) * 4
     assert c["bytes_per_rank"] == n and c["ring_bytes_per_rank"] == n
+    # the ranges tile the flat buffer; fine / coarse meet at level 8's start
+    cut = 2 * int(LY.grid_levels(0.5)["offset"][8])
+    assert rg["coarse"] == [0, cut] and rg["fine"][0] == cut
+    assert rg["fine"][1] == rg["rest"][0] and rg["rest"][1] * 4 == n
 
 
 def test_bench_world_mismatch_fails():
@@ -176,3 +183,22 @@ def test_bench_world_mismatch_fails():
                          env=env, capture_output=True, text=True, timeout=240)
     assert out.returncode != 0
     assert "--gpus 4 but the process group has 2" in out.stderr
+
+
+def test_step_ranges_tile_the_buffer():
+    """dist.step_ranges: MLP + gate, fine grid levels, coarse grid levels --
+    disjoint, covering the flat buffer exactly, the cut on a level boundary
+    (split 0: the whole grid in "fine")."""
+    from radnerf_amd import layout as LY
+    for scale in (0.5, 16.0):
+        lv = LY.grid_levels(scale)
+        n_grid = 2 * int(lv["n_entries"])
+        ar = rdist.GradAllReduce([torch.zeros(n_grid), torch.zeros(3, LY.FIELD_PARAMS),
+                                  torch.zeros(LY.gate_params(3))], "cpu")
+        for split in (0, 1, 8, 15):
+            rg = rdist.step_ranges(ar, lv["offset"], split)
+            seen = torch.zeros(ar.flat.numel(), dtype=torch.int32)
+            for a, b in rg.values():
+                seen[a:b] += 1
+            assert bool((seen == 1).all()), (scale, split)
+            assert rg["coarse"][1] == (2 * int(lv["offset"][split]) if split else 0)

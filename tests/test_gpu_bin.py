@@ -26,11 +26,21 @@ from test_gpu_ml import FX_LEVEL_TOL, _run, _setup, check_fx_vs_fp32
 pytestmark = pytest.mark.gpu
 
 
-def _pack(idx, q0, q1, lay):
+def _field(q):
+    """the e5m17 field of record values q (rn_grid_record_encode) and the exact
+    value the sum pass adds for it"""
+    q = np.ascontiguousarray(q, np.float32)
+    f = np.zeros(len(q), np.uint32)
+    v = np.zeros(len(q), np.int64)
+    lib().grid_record_encode(q.ctypes.data, len(q), f.ctypes.data)
+    lib().grid_record_decode(f.ctypes.data, len(q), v.ctypes.data)
+    return f, v
+
+
+def _pack(idx, f0, f1, lay):
     ib, vb = lay["idx_bits"], lay["v_bits"]
-    m = (1 << vb) - 1
-    return (idx.astype(np.uint64) | ((q0.astype(np.int64) & m).astype(np.uint64) << np.uint64(ib))
-            | ((q1.astype(np.int64) & m).astype(np.uint64) << np.uint64(ib + vb))).view(np.int64)
+    return (idx.astype(np.uint64) | (f0.astype(np.uint64) << np.uint64(ib))
+            | (f1.astype(np.uint64) << np.uint64(ib + vb))).view(np.int64)
 
 
 @pytest.mark.parametrize("in_place", [True, False])
@@ -41,7 +51,7 @@ def test_bin_sum_exact_on_synthetic_pages(cuda, in_place):
     scale = 16.0
     lv = LY.grid_levels(scale)
     rng = np.random.default_rng(7)
-    vmax = (1 << (lay["v_bits"] - 1)) - 1
+    vmax = 2.0 ** 40          # record values over most of the e5m17 range
     pages, metas, per = [], [], []
     for l in range(16):
         hs = int(lv["hsize"][l])
@@ -50,10 +60,12 @@ def test_bin_sum_exact_on_synthetic_pages(cuda, in_place):
         if l == 15:                         # one hot entry and the range ends
             idx[: n // 4] = hs - 1
             idx[n // 4: n // 4 + 10] = 0
-        q0 = rng.integers(-vmax, vmax + 1, n)
-        q1 = rng.integers(-vmax, vmax + 1, n)
+        # log-uniform magnitudes (1 unit .. 2^30), random signs; a few zeros
+        mag = np.exp2(rng.uniform(0, np.log2(vmax), (2, n))) * (rng.random((2, n)) > 0.01)
+        sg = np.where(rng.random((2, n)) < 0.5, -1.0, 1.0)
+        (f0, q0), (f1, q1) = _field(mag[0] * sg[0]), _field(mag[1] * sg[1])
         per.append((idx, q0, q1))
-        rec = _pack(idx, q0, q1, lay)
+        rec = _pack(idx, f0, f1, lay)
         fill = int(rng.integers(PAGE // 2, PAGE + 1))                # partial pages
         for a in range(0, n, fill):
             c = rec[a:a + fill]
@@ -80,9 +92,12 @@ def test_bin_sum_exact_on_synthetic_pages(cuda, in_place):
     st = torch.cuda.current_stream().cuda_stream
     L.grid_bin(lv["hsize"].ctypes.data, ctl.data_ptr(), meta.data_ptr(), pin.data_ptr(), pout.data_ptr(), desc.data_ptr(),
                lpages.data_ptr(), pool, 64, st)
-    L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, ctl.data_ptr(),
-               desc.data_ptr(), lpages.data_ptr(), pout.data_ptr(), pool, sc_t.data_ptr(), None,
-               grad.data_ptr(), st)
+    # in two launches (fine levels first, as the data-parallel step runs it
+    # to start their all-reduce early): the same sums
+    for lo, hi in ((7, 16), (0, 7)):
+        L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, ctl.data_ptr(),
+                   desc.data_ptr(), lpages.data_ptr(), pout.data_ptr(), pool, sc_t.data_ptr(), None,
+                   grad.data_ptr(), lo, hi, st)
     got = grad.cpu().numpy().reshape(-1, 2)
     want = grad0.copy().reshape(-1, 2)
     for l, (idx, q0, q1) in enumerate(per):
@@ -160,9 +175,136 @@ def test_binned_pool_overflow_redo_then_grows(cuda):
     assert int(redo[0]) == 1
     for x, y in zip(g_redo, g32):
         assert float((x - y).norm() / y.norm().clamp_min(1e-30)) <= 1e-5
-    torch.cuda.synchronize()
+    # the pool grows from the page count of the backward BIN_LAG (2) back,
+    # whatever the host's lead: the next step still overflows (redone in
+    # fp32, deterministically), the one after runs binned on the grown pool
+    _, g_redo2 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    assert int(redo[0]) == 1 and r.ws._bin["pages"] == pool["pages"]
     _, gb = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)   # grown
     assert r.ws._bin["pages"] > pool["pages"]
     assert int(redo[0]) == 0
     check_fx_vs_fp32(m, gb, g32, r, "binned after pool growth")
     assert FX_LEVEL_TOL > 0
+
+
+def _pool(cuda, lay, pool, pages, metas, canary=64):
+    """the pass buffers with `canary` guard elements past each one's end"""
+    PAGE = lay["page"]
+    i32 = dict(device=cuda, dtype=torch.int32)
+    C = canary
+    buf = dict(
+        ctl=torch.zeros(lay["ctl_bytes"] // 4 + C, **i32),
+        meta=torch.full((pool + C,), 0x5a5a5a5a, **i32),
+        pin=torch.full((pool * PAGE + C,), 0x3c3c3c3c3c3c3c3c, device=cuda, dtype=torch.int64),
+        pout=torch.full((pool * PAGE + C,), 0x3c3c3c3c3c3c3c3c, device=cuda, dtype=torch.int64),
+        desc=torch.full((pool * lay["bins"] + C,), 0x5a5a5a5a, **i32),
+        lpages=torch.full((16 * pool + C,), 0x5a5a5a5a, **i32))
+    buf["ctl"][lay["ctl_bytes"] // 4:] = 0x5a5a5a5a
+    buf["ctl"][0] = len(pages)
+    buf["meta"][:len(metas)] = torch.tensor(metas, **i32)
+    if pages:
+        buf["pin"][:len(pages) * PAGE] = torch.from_numpy(np.stack(pages).ravel())
+    return buf
+
+
+def _canaries_intact(buf, lay, pool):
+    PAGE = lay["page"]
+    ends = dict(ctl=lay["ctl_bytes"] // 4, meta=pool, pin=pool * PAGE, pout=pool * PAGE,
+                desc=pool * lay["bins"], lpages=16 * pool)
+    for k, e in ends.items():
+        t = buf[k][e:]
+        want = 0x3c3c3c3c3c3c3c3c if t.dtype == torch.int64 else 0x5a5a5a5a
+        assert bool((t == want).all()), k
+
+
+@pytest.mark.parametrize("case", ["clean", "meta_count", "meta_level", "index"])
+def test_bin_pass_refuses_corrupt_inputs(cuda, case):
+    """the bin pass trusted page_meta (count and level) and
+    every record's entry index; a corrupt one indexed LDS and HBM out of
+    bounds.  Now a page whose meta names a level >= 16 or more than 8192
+    records, or a record whose index lies outside its level, is refused: the
+    GbCtl fault word is set, rn_grid_binned_fold raises the redo flag, the sum
+    pass adds nothing, and no byte past any buffer changes.  Control: the same
+    pages without the corruption fold exactly."""
+    L = lib()
+    lay = L.bin_layout()
+    PAGE = lay["page"]
+    scale = 16.0
+    lv = LY.grid_levels(scale)
+    hs = lv["hsize"]
+    rng = np.random.default_rng(11)
+    pages, metas, per = [], [], []
+    for l in (2, 9, 15):
+        n = 3000
+        idx = rng.integers(0, int(hs[l]), n)
+        (f0, q0), (f1, q1) = _field(rng.integers(-500, 500, n)), _field(rng.integers(-500, 500, n))
+        pg = np.zeros(PAGE, np.int64)
+        pg[:n] = _pack(idx, f0, f1, lay)
+        pages.append(pg); metas.append(l | (n << 8)); per.append((l, idx, q0, q1))
+    if case == "meta_count":
+        metas[1] = 9 | ((PAGE + 1000) << 8)
+    elif case == "meta_level":
+        metas[1] = 20 | (3000 << 8)
+    elif case == "index":
+        pages[0][17] = _pack(np.array([int(hs[2]) + 5]), *_field(np.array([7]))[:1],
+                             *_field(np.array([7]))[:1], lay)[0]
+    pool = 4
+    buf = _pool(cuda, lay, pool, pages, metas)
+    sc = torch.full((2, 16), 1.0, device=cuda)
+    stats = torch.zeros(160, device=cuda, dtype=torch.int32)
+    redo = torch.zeros(1, device=cuda, dtype=torch.int32)
+    n_el = 2 * int(lv["n_entries"])
+    grad = torch.zeros(n_el + 64, device=cuda)
+    st = torch.cuda.current_stream().cuda_stream
+    L.grid_binned_fold(lv["offset"].ctypes.data, hs.ctypes.data, buf["ctl"].data_ptr(),
+                       buf["meta"].data_ptr(), buf["pin"].data_ptr(), buf["pout"].data_ptr(),
+                       buf["desc"].data_ptr(), buf["lpages"].data_ptr(), pool, sc[0].data_ptr(),
+                       sc[1].data_ptr(), stats.data_ptr(), redo.data_ptr(), grad.data_ptr(), st)
+    torch.cuda.synchronize()
+    _canaries_intact(buf, lay, pool)
+    assert bool((grad[n_el:] == 0).all())
+    fault = int(buf["ctl"][17])
+    if case == "clean":
+        assert fault == 0 and int(redo[0]) == 0
+        g = grad[:n_el].view(-1, 2).cpu().numpy()
+        for l, idx, q0, q1 in per:
+            off = int(lv["offset"][l])
+            a0 = np.zeros(int(hs[l]), np.int64)
+            np.add.at(a0, idx, q0)
+            assert np.array_equal(g[off:off + int(hs[l]), 0], a0.astype(np.float32))
+    else:
+        assert fault == (2 if case == "index" else 1), fault
+        assert int(redo[0]) == 1
+        assert float(grad[:n_el].abs().max()) == 0.0          # the sum pass added nothing
+
+
+def test_bin_pass_without_ctl_reset_stays_in_bounds(cuda):
+    """The round-4 fault (tools/bin_probe.py, an ablation loop that re-ran the
+    bin pass without zeroing GbCtl): the level page counters kept counting,
+    so the second pass wrote level_pages slots past its level's row -- for
+    level 15 past the end of the buffer.  Now a slot >= pool_pages is refused
+    (fault bit 4) and nothing is written past the list."""
+    L = lib()
+    lay = L.bin_layout()
+    PAGE = lay["page"]
+    lv = LY.grid_levels(16.0)
+    hs = lv["hsize"]
+    rng = np.random.default_rng(5)
+    pages, metas = [], []
+    for _ in range(4):                                   # every page: level 15
+        n = 1000
+        f = _field(rng.integers(-9, 9, n))[0]
+        pg = np.zeros(PAGE, np.int64)
+        pg[:n] = _pack(rng.integers(0, int(hs[15]), n), f, f, lay)
+        pages.append(pg); metas.append(15 | (n << 8))
+    pool = 4
+    buf = _pool(cuda, lay, pool, pages, metas)
+    st = torch.cuda.current_stream().cuda_stream
+    for _ in range(2):                                   # the second run: no reset
+        L.grid_bin(hs.ctypes.data, buf["ctl"].data_ptr(), buf["meta"].data_ptr(),
+                   buf["pin"].data_ptr(), buf["pout"].data_ptr(), buf["desc"].data_ptr(),
+                   buf["lpages"].data_ptr(), pool, 64, st)
+    torch.cuda.synchronize()
+    _canaries_intact(buf, lay, pool)
+    assert int(buf["ctl"][1 + 15]) == 8                  # counted on ...
+    assert int(buf["ctl"][17]) & 4                       # ... but refused

@@ -140,29 +140,38 @@ def test_fx_entry_wrap_sets_redo(cuda):
     assert int(stats.abs().max()) == 0
 
 
-def test_fx_per_entry_agreement(cuda, capsys):
-    """fixed point per ENTRY, not only per-level norms.  One C3-
-    shaped step (B = 2048, K = 2) fixed point vs fp32 on the hashed levels:
-    the share of entries non-zero in fp32 but zero in fixed point, and the
-    sign agreement of the entries whose fp32 gradient is above the level's
-    fixed-point unit (1 / 2^e_l); then 3 FusedAdam steps (eps 1e-15, as
-    train_ml.py) from the same start with either gradient: the parameter
-    updates per hashed level.  The measured values are printed (DESIGN.md
-    §2 quotes them); the bars hold what a per-entry deviation may not exceed."""
+# (B, K, scale): C3's shape (int32 fixed point, atomics), C4's branch (K = 4,
+# scale 16, exponential steps) and a C5-shaped one (K = 8, scale 16), both on
+# the binned scatter (the default at scale 16)
+PER_ENTRY_SHAPES = [(2048, 2, 0.5), (4096, 4, 16.0), (2048, 8, 16.0)]
+
+
+@pytest.mark.parametrize("B,K,scale", PER_ENTRY_SHAPES)
+def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
+    """fixed point per ENTRY, not only per-level norms.  One
+    step fixed point vs fp32 over every level: the share of entries non-zero
+    in fp32 but zero in fixed point, and the sign agreement of the entries
+    whose fp32 gradient is above the level's fixed-point unit (1 / 2^e_l);
+    then 3 FusedAdam steps (eps 1e-15, as train_ml.py) from the same start
+    with either gradient: the parameter updates per level.  The measured
+    values are printed (DESIGN.md §2 quotes them); the bars hold what a
+    per-entry deviation may not exceed."""
     from radnerf_amd.optim import FusedAdam
-    B, K = 2048, 2
-    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
-    hashed, lv = _hashed(0.5)
-    _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)              # scales
+    assert r.grid_fx and r.grid_bin == (scale > 0.5)
+    lv = LY.grid_levels(scale)
+    _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)              # scales
     unit = (1.0 / r.ws._fx[1][r.ws.fx_i].clamp_min(1e-30)).cpu()
-    _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
+    _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    assert int(r.ws._fx[3][0]) == 0                                         # no redo
     r.grid_fx = False
-    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     r.grid_fx = True
     a_all, b_all = gfx[0].view(-1, 2), g32[0].view(-1, 2)
     lost, n_nz, agree, n_big = 0, 0, 0, 0
-    for l in hashed:
+    for l in range(16):
         a, b = _level(a_all, lv, l), _level(b_all, lv, l)
         nz = b != 0
         n_nz += int(nz.sum())
@@ -171,25 +180,41 @@ def test_fx_per_entry_agreement(cuda, capsys):
         n_big += int(big.sum())
         agree += int((torch.sign(a[big]) == torch.sign(b[big])).sum())
     f_lost, f_agree = lost / max(n_nz, 1), agree / max(n_big, 1)
-    # Adam: 3 steps from the same parameters with each gradient mode
+    # Adam: 3 steps from the same parameters with each gradient mode, and fp32
+    # again with the rays in reverse order (the same gradient, summed in
+    # another order): with eps = 1e-15 an entry whose records cancel to
+    # rounding noise still takes an lr-sized step, so fp32 differs from itself
+    # under reordering -- the floor any summation of these records meets
     p0 = m.xyz_encoder.params.detach().clone()
+    rev = (o[::-1].copy(), d[::-1].copy(), noise[:, ::-1].copy(),
+           tuple(x[::-1].copy() for x in seeds))
     deltas = {}
-    for mode in (True, False):
+    for mode in ("fx", "fp32", "fp32_reordered"):
         with torch.no_grad():
             m.xyz_encoder.params.copy_(p0)
         opt = FusedAdam([m.xyz_encoder.params], lr=1e-2, eps=1e-15)
-        r.grid_fx = mode
+        r.grid_fx = mode == "fx"
+        oo, dd, nn, ss = rev if mode == "fp32_reordered" else (o, d, noise, seeds)
         for _ in range(3):
-            _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
+            _run(ml_render_fused, m, g, oo, dd, nn, ss, cuda, esf)
             opt.step()
         deltas[mode] = (m.xyz_encoder.params.detach() - p0).view(-1, 2)
     r.grid_fx = True
-    rel = max(float((_level(deltas[True], lv, l) - _level(deltas[False], lv, l)).norm() /
-                    _level(deltas[False], lv, l).norm().clamp_min(1e-30)) for l in hashed)
+
+    def upd(x, y):
+        return [float((_level(deltas[x], lv, l) - _level(deltas[y], lv, l)).norm() /
+                      _level(deltas[y], lv, l).norm().clamp_min(1e-30)) for l in range(16)]
+    rels, floor = upd("fx", "fp32"), upd("fp32_reordered", "fp32")
+    rel = max(rels)
     with capsys.disabled():
-        print(f"\nfx per entry: {f_lost:.4%} of the non-zero fp32 entries are 0 in fixed point; "
+        print(f"\nfx per entry B{B} K{K} s{scale} ({'binned' if r.grid_bin else 'int32'}): "
+              f"{f_lost:.4%} of the non-zero fp32 entries are 0 in fixed point; "
               f"sign agreement above one unit {f_agree:.5%} ({n_big} entries); "
-              f"3 Adam steps: per-level update difference max {rel:.3e}")
+              f"3 Adam steps: per-level update difference max {rel:.3e} "
+              f"(level {int(np.argmax(rels))}); fp32 vs fp32 of the reversed rays max "
+              f"{max(floor):.3e}")
+        print("  per level fx-fp32 " + " ".join(f"{x:.3f}" for x in rels))
+        print("  per level fp32-fp32 reordered " + " ".join(f"{x:.3f}" for x in floor))
     assert f_agree >= 0.999
     assert f_lost <= 0.05
     assert rel <= 0.04

@@ -253,6 +253,35 @@ def test_fused_full_size_properties(cuda, B, K, scale):
     assert np.all(valid[perm]) and len(np.unique(perm)) == total
 
 
+@pytest.mark.parametrize("B,K,scale", [(8192, 2, 0.5), (4096, 4, 16.0), (8192, 8, 16.0)])
+def test_full_size_fx_vs_fp32(cuda, B, K, scale):
+    """the default grid gradient at the full per-GPU sizes
+    -- C3 (int32 fixed point), C4 and C5 (binned; C5 with 2048-sample chunks,
+    hundreds of pages per level and the pool sized from the first step) --
+    against the same step's fp32-atomic gradient, per level (FX_LEVEL_TOL),
+    MLP and gate gradients unchanged; then two more default steps with
+    identical inputs give identical bits (exact integer sums)."""
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    assert r.grid_fx and r.grid_bin == (scale > 0.5)
+    _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)        # fp32: measures the scales
+    _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    r.grid_fx = False
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    r.grid_fx = True
+    n_fx = check_fx_vs_fp32(m, gfx, g32, r, f"full size B{B} K{K} s{scale}")
+    assert n_fx == 16
+    if r.grid_bin:
+        pool = r.ws._bin
+        assert 0 < int(pool["ctl"][0]) <= pool["pages"]
+        assert 0 < int(pool["ctl"][1:17].sum()) <= int(pool["ctl"][0])   # pages with records listed
+    _, gb = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    _, gc = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    assert int(r.ws._fx[3][0]) == 0
+    assert torch.equal(gb[0], gc[0])
+
+
 def _merged_vs_split(cuda, B, K, scale, p=0.5):
     esf = 1 / 256 if scale > 0.5 else 0.0
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale, p=p)

@@ -106,3 +106,25 @@ def test_reference_dropin_module_names():
     from radnerf_amd import custom_functions as cf
     for n in ("RayAABBIntersector", "RayMarcher", "VolumeRenderer", "TruncExp"):
         assert issubclass(getattr(cf, n), torch.autograd.Function)
+
+
+def test_product_library_has_one_code_path():
+    """timing-study variants (the merged backward's ABL
+    instantiations, the sum pass's ABL / PROF / BIS and the bin pass's
+    512 / 256-thread forms) live only in librn_abl.so; librn.so holds one
+    instantiation of each of those kernels per production mode."""
+    import os
+    import re
+    from radnerf_amd import _lib
+    names = {}
+    for key, path in (("prod", _lib.LIB_PATH), ("abl", _lib.ABLATION_LIB_PATH)):
+        data = open(path, "rb").read()
+        names[key] = set(re.findall(rb"_ZN12_GLOBAL__N_1\d+(k_grid_sum|k_grid_bin|k_field_bwd_merged)I([A-Za-z0-9_]*?)EEEv", data))
+        assert os.path.getsize(path) > 0
+    prod = {(k.decode(), t.decode()) for k, t in names["prod"]}
+    assert ("k_grid_sum", "Li0ELb0ELi0") in prod and ("k_grid_bin", "Li1024ELb0") in prod
+    assert not [x for x in prod if x[0] == "k_grid_sum" and x[1] != "Li0ELb0ELi0"], prod
+    assert not [x for x in prod if x[0] == "k_grid_bin" and x[1] != "Li1024ELb0"], prod
+    assert not [x for x in prod if x[0] == "k_field_bwd_merged" and "Lb1E" in x[1] + "E"], prod
+    abl = {(k.decode(), t.decode()) for k, t in names["abl"]}
+    assert len(abl) > len(prod)

@@ -45,7 +45,7 @@ def test_merged_entry_points_validate_without_gpu():
     with pytest.raises(RuntimeError, match="bad sizes"):
         L.grid_bin(*[V] * 7, 0, 2048, None)
     with pytest.raises(RuntimeError, match="null pointer"):
-        L.grid_sum(*P[:6], 16, None, None, None, None)
+        L.grid_sum(*P[:6], 16, None, None, None, 0, 16, None)
     with pytest.raises(RuntimeError, match="null pointer"):
         L.grid_binned_fold(*P[:8], 16, *P[:6])
     assert L.version() == _lib.ABI_VERSION
@@ -65,7 +65,8 @@ def test_abi_constants_match_the_header():
     assert int(re.search(r"#define RN_ABI_VERSION (\d+)", hdr).group(1)) == _lib.ABI_VERSION
     assert int(re.search(r"#define RN_FX_STATS_BYTES (\d+)", hdr).group(1)) == fused.FX_STATS_BYTES
     lay = _lib.lib().bin_layout()
-    assert lay == dict(page=8192, bins=256, slice=4096, ctl_bytes=128, idx_bits=20, v_bits=22)
+    assert lay == dict(page=8192, bins=256, slice=4096, ctl_bytes=128, idx_bits=20, v_bits=22,
+                       m_bits=17, target_bits=38)
 
 
 def test_grid_bin_and_sum_reject_oversized_levels():
@@ -77,7 +78,7 @@ def test_grid_bin_and_sum_reject_oversized_levels():
         L.grid_bin(hs.ctypes.data, *[V] * 6, 16, 2048, None)
     off = np.zeros(16, np.uint32)
     with pytest.raises(RuntimeError, match="level too large"):
-        L.grid_sum(off.ctypes.data, hs.ctypes.data, *[V] * 4, 16, V, None, V, None)
+        L.grid_sum(off.ctypes.data, hs.ctypes.data, *[V] * 4, 16, V, None, V, 0, 16, None)
 
 
 def test_grid_slice_bits_rule():
@@ -100,3 +101,47 @@ def test_grid_slice_bits_rule():
             assert out[0] == 6 and out[-1] == 12     # 4096 entries in 64s; 2^19 in 4096s
     with pytest.raises(RuntimeError, match="level too large"):
         L.grid_slice_bits(np.full(16, 1 << 21, np.uint32).ctypes.data, np.zeros(16, np.int32).ctypes.data)
+
+
+def _encode(x):
+    import numpy as np
+    L = _lib.lib()
+    x = np.ascontiguousarray(x, np.float32)
+    f = np.zeros(len(x), np.uint32)
+    L.grid_record_encode(x.ctypes.data, len(x), f.ctypes.data)
+    v = np.zeros(len(x), np.int64)
+    L.grid_record_decode(f.ctypes.data, len(x), v.ctypes.data)
+    return f, v
+
+
+def test_grid_record_e5m17_format():
+    """The binned scatter's record value (csrc/rn_bin.h gb_encode, VERDICT r04
+    item 1): exact to one unit below 2^15 units (e = 0, m = rint(x)); above,
+    14 significant bits past the leading one (relative error <= 2^-15);
+    every |x| < 2^46 representable, sign-symmetric, monotone; the 22-bit
+    field is mantissa [0, 17) | exponent << 17."""
+    import numpy as np
+    rng = np.random.default_rng(3)
+    small = rng.uniform(-32767.4, 32767.4, 20000).astype(np.float32)
+    f, v = _encode(small)
+    assert np.array_equal(v, np.rint(small).astype(np.int64))
+    assert np.all(f >> 17 == 0) and np.all(f < (1 << 22))
+    # the whole range, log-uniform, both signs
+    mag = np.exp2(rng.uniform(-30, 45.999, 200000)).astype(np.float32)
+    x = np.where(rng.random(len(mag)) < 0.5, -mag, mag).astype(np.float32)
+    f, v = _encode(x)
+    assert np.all(f < (1 << 22))
+    xd = x.astype(np.float64)
+    err = np.abs(v - xd)
+    big = np.abs(xd) >= 32768.0
+    assert np.all(err[~big] <= 0.5)
+    assert np.all(err[big] / np.abs(xd[big]) <= 2.0 ** -15)
+    f2, v2 = _encode(-x)
+    assert np.array_equal(v2, -v)
+    o = np.argsort(xd)
+    assert np.all(np.diff(v[o]) >= 0)                  # monotone
+    # just below 2^46 units: representable, rounded to 2^-15 relative
+    edge = np.array([2.0 ** 46 * (1 - 2.0 ** -24), -(2.0 ** 46) * (1 - 2.0 ** -24)], np.float32)
+    f, v = _encode(edge)
+    assert np.array_equal(v, np.array([2 ** 46, -(2 ** 46)], np.int64))
+    assert np.all(f >> 17 == 31)

@@ -19,7 +19,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from radnerf_amd import synthetic as S  # noqa: E402
-from radnerf_amd._lib import lib  # noqa: E402
+from radnerf_amd._lib import lib, use_ablation_build  # noqa: E402
+
+use_ablation_build()        # rn_set_debug_flags switches live only in librn_abl.so
 from radnerf_amd.fused import FusedMLRenderer  # noqa: E402
 from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 
@@ -53,7 +55,7 @@ def main():
         for _ in range(2):         # the first backward is fp32 and sets the scales
             _, _, _, gt, _ = rr.forward(o, d, d, nz, bg, 1e-4, esf)
             rr.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
-        rr.trace = {"field_bwd", "fx_fold"}
+        rr.trace = {"field_bwd", "fx_fold", "fx_bin", "fx_sum", "fx_redo"}
         rens[key] = rr
     kern = {}
     L = lib()
@@ -94,7 +96,7 @@ def main():
             if int(f.lstrip("fsixa")) & 4096:
                 cyc = (ctypes.c_ulonglong * 8)()
                 L.debug_cycles(ctypes.cast(cyc, ctypes.c_void_p).value)
-                phases.setdefault(f, []).append([int(c) for c in cyc[:4]])
+                phases.setdefault(f, []).append([int(c) for c in cyc[:8]])
         L.set_debug_flags(0)
         r = rens[""]
         a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -113,11 +115,19 @@ def main():
            "kernel_ms": {f: {k: round(float(np.median(v)), 4) for k, v in kv.items()}
                          for f, kv in kern.items()},
            # flag 4096: summed wave cycles per phase (MLP, staging, walk, chunk
-           # tails), median over rounds, as fractions of their sum
+           # tails), median over rounds, as fractions of their sum; inside the
+           # MLP phase: model switches, forward recompute (its loads waited
+           # for), bwd_window, row stores (fractions of the MLP phase)
            "phases": {f: dict(zip(("mlp", "staging", "walk", "tail"),
                                   [round(float(x), 4) for x in
-                                   (np.median(np.array(v), 0) / np.median(np.array(v), 0).sum())]))
-                      for f, v in phases.items()}}
+                                   (np.median(np.array(v)[:, :4], 0) /
+                                    np.median(np.array(v)[:, :4], 0).sum())]))
+                      for f, v in phases.items()},
+           "mlp_phases": {f: dict(zip(("switch", "forward", "bwd_window", "rows"),
+                                      [round(float(x), 4) for x in
+                                       (np.median(np.array(v)[:, 4:], 0) /
+                                        max(1.0, float(np.median(np.array(v)[:, 0]))))]))
+                          for f, v in phases.items()}}
     print(json.dumps(out))
 
 

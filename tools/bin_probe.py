@@ -22,17 +22,19 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "rad-nerf_amd")]
 from radnerf_amd import layout as LY  # noqa: E402
-from radnerf_amd._lib import lib  # noqa: E402
+from radnerf_amd._lib import lib, use_ablation_build  # noqa: E402
+
+use_ablation_build()        # rn_set_debug_flags switches live only in librn_abl.so
 
 
 def _layout():
     import ctypes
-    out = (ctypes.c_int32 * 6)()
+    out = (ctypes.c_int32 * 8)()
     lib().grid_bin_layout(out)
     return list(out)
 
 
-PAGE, MAX_BINS, SLICE, CTL_BYTES, IDX_BITS, V_BITS = _layout()
+PAGE, MAX_BINS, SLICE, CTL_BYTES, IDX_BITS, V_BITS = _layout()[:6]
 
 # records / sample per level (tools/records_sim.py: K 8 scale 16 B 1024, chunk 2048)
 REC_C5 = [0.16, 0.25, 0.39, 0.61, 0.96, 1.51, 2.31, 3.36, 4.51, 5.56, 6.38, 6.96, 7.35, 7.60,
@@ -40,10 +42,17 @@ REC_C5 = [0.16, 0.25, 0.39, 0.61, 0.96, 1.51, 2.31, 3.36, 4.51, 5.56, 6.38, 6.96
 SHAPES = {"c5": (16.0, 6227661, REC_C5)}
 
 
+def _field(q):
+    """e4m18 fields of integer record values (exact below 2^16 units)"""
+    q = np.ascontiguousarray(q, np.float32)
+    f = np.zeros(len(q), np.uint32)
+    lib().grid_record_encode(q.ctypes.data, len(q), f.ctypes.data)
+    return f.astype(np.uint64)
+
+
 def pack(idx, q0, q1):
-    m = (1 << V_BITS) - 1
-    return (idx.astype(np.uint64) | ((q0.astype(np.int64) & m).astype(np.uint64) << np.uint64(IDX_BITS))
-            | ((q1.astype(np.int64) & m).astype(np.uint64) << np.uint64(IDX_BITS + V_BITS)))
+    return (idx.astype(np.uint64) | (_field(q0) << np.uint64(IDX_BITS))
+            | (_field(q1) << np.uint64(IDX_BITS + V_BITS)))
 
 
 class Pool:
@@ -137,7 +146,7 @@ def main():
         ev[1].record(st)
         L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
                    pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
-                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), 0, 16, sp)
         ev[2].record(st)
         torch.cuda.synchronize()
         if it == 0:
@@ -159,7 +168,7 @@ def main():
             ev[1].record(st)
             L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
                        pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
-                       pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+                       pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), 0, 16, sp)
             ev[2].record(st)
             torch.cuda.synchronize()
             t.append(ev[1].elapsed_time(ev[2]))
@@ -173,7 +182,7 @@ def main():
     ev[1].record(st)
     L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
                pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
-               pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+               pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), 0, 16, sp)
     ev[2].record(st)
     torch.cuda.synchronize()
     L.set_debug_flags(0)
@@ -196,7 +205,7 @@ def main():
         ev[1].record(st)
         L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
                    pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
-                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), 0, 16, sp)
         ev[2].record(st)
         torch.cuda.synchronize()
         t.append(ev[1].elapsed_time(ev[2]))
@@ -235,7 +244,7 @@ def main():
         ev[1].record(st)
         L.grid_sum(lv["offset"].ctypes.data, lv["hsize"].ctypes.data, pool.ctl.data_ptr(),
                    pool.desc.data_ptr(), pool.lpages.data_ptr(), pool.pout.data_ptr(),
-                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), sp)
+                   pool.pool_pages, scale_t.data_ptr(), None, grad.data_ptr(), 0, 16, sp)
         ev[2].record(st)
         torch.cuda.synchronize()
         t.append(ev[1].elapsed_time(ev[2]))

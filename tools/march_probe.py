@@ -12,7 +12,9 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from radnerf_amd import synthetic as S  # noqa: E402
-from radnerf_amd._lib import lib  # noqa: E402
+from radnerf_amd._lib import lib, use_ablation_build  # noqa: E402
+
+use_ablation_build()        # rn_set_debug_flags switches live only in librn_abl.so
 from radnerf_amd.fused import FusedMLRenderer  # noqa: E402
 from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 

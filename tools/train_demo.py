@@ -76,7 +76,8 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
             acc_rgb, n_acc = 0.0, 0
     torch.cuda.synchronize()
     params = torch.cat([m.xyz_encoder.params.detach().view(-1), m.mlp_params.detach().view(-1)])
-    return {"grid_fx": grid_fx, "seconds": round(time.time() - t0, 2), "curve": curve,
+    return {"grid_fx": grid_fx, "binned": bool(grid_fx and tr.renderer.grid_bin),
+            "seconds": round(time.time() - t0, 2), "curve": curve,
             "fx_redo_steps": redo_steps if grid_fx else None,
             "final_psnr": curve[-1]["psnr"], "params": params}
 
