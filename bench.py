@@ -358,7 +358,10 @@ def main():
     ar.reset_timing()
     # timed region: HIP events only around the roofline kernel (an event pair
     # per launch costs ~5 us of queue time; all twelve would add ~2.5 %)
-    r.trace = {"field_bwd"}
+    binned_run = bool(getattr(r, "grid_bin", False) and r.grid_fx and not args.split_bwd)
+    # (binned scatter: the fold's two event spans too -- the roofline covers
+    # field_bwd + bin + sum)
+    r.trace = {"field_bwd", "fx_bin", "fx_sum"} if binned_run else {"field_bwd"}
     r.events = {}
     if world > 1:
         dist.barrier()
@@ -370,7 +373,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    bwd_live = r.kernel_times_ms()["field_bwd"]
+    live = r.kernel_times_ms()
+    bwd_live = live["field_bwd"]
     comm = None
     if world > 1:
         # the collectives of the timed steps, then the same steps without them:
@@ -412,6 +416,9 @@ def main():
     r.trace = False
     kt = r.kernel_times_ms()
     kt["field_bwd"] = bwd_live
+    for k_ in ("fx_bin", "fx_sum"):             # the binned fold, timed in the headline region
+        if k_ in live:
+            kt[k_] = live[k_]
     # gate_bwd runs on a side stream beside field_bwd (hidden there, but its
     # events then span the wait for CUs): its own duration, in line
     at = r.gate_bwd_at
@@ -625,7 +632,8 @@ def main():
                 atom_req = tj.get("field_bwd_atomic_requests")
         except (OSError, ValueError, AttributeError):
             traffic = None
-    roofline = {"kernel": "field_bwd", "bound": "hbm", "achieved": round(achieved, 1),
+    roofline = {"kernel": "field_bwd (k_field_bwd_merged)", "bound": "hbm",
+                "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic, "traffic_source": pmc_key if traffic else None,
                 "algorithmic_bytes_per_sample": FIELD_BWD_BYTES_PER_SAMPLE,
@@ -671,6 +679,24 @@ def main():
             "fold_frac": round(24 * recs / (fold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "fold_traffic": (tj or {}).get("grid_fold_bytes_per_launch"),
             "walk_store_bytes": 8 * recs}
+        # the scatter finishes in the fold: the roofline covers the merged
+        # backward + bin + check + sum (algorithmic bytes as for field_bwd alone,
+        # 1,064 per sample; traffic = the walk's + the fold's PMC bytes); the
+        # merged backward alone stays in field_bwd_only
+        if fold_ms == fold_ms:
+            only = {k_: roofline[k_] for k_ in ("kernel", "achieved", "frac", "traffic",
+                                                "avg_launch_ms")}
+            tot_ms = bwd_ms + fold_ms
+            ach = samples_per_step_rank * FIELD_BWD_BYTES_PER_SAMPLE / (tot_ms * 1e-3) / 1e9
+            ft = (tj or {}).get("grid_fold_bytes_per_launch")
+            roofline.update({
+                "kernel": "field_bwd + binned fold (k_field_bwd_merged, k_grid_bin, k_fx_check, "
+                          "k_grid_sum)",
+                "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                "avg_launch_ms": round(tot_ms, 4),
+                "traffic": (round((traffic or 0) + ft * samples_per_step_rank / pmc_samples)
+                            if traffic and ft and pmc_samples else None),
+                "field_bwd_only": only})
 
     rgb_linf = None
     cpu_base = None

@@ -517,12 +517,12 @@ class FusedMLRenderer:
                                  pool["desc"].data_ptr(), pool["lpages"].data_ptr(), pool["pages"],
                                  cur.data_ptr(), nxt.data_ptr(), stats.data_ptr(),
                                  redo.data_ptr(), st)
+                self._ev_close(span)
                 # the pages this backward took, read back without a sync
                 # (_bin_pool reads it BIN_LAG backwards later)
                 seen = self._bin_seen(w)
                 seen[0].copy_(pool["ctl"][:1], non_blocking=True)
                 seen[1].record(torch.cuda.current_stream(grid_grad.device))
-                self._ev_close(span)
                 fx_redo()
                 span = self._ev_open("fx_sum")
                 split = max(0, min(16, int(self.grid_split_level))) if self.after_grid_levels else 0
