@@ -329,7 +329,8 @@ def main():
             grid_early[0] = a
 
     r.after_field_bwd = early_bucket
-    r.after_grid_levels = grid_levels_ready
+    # (one rank: no collective to overlap, the fold sums every level in one launch)
+    r.after_grid_levels = grid_levels_ready if world > 1 else None
 
     def step(i):
         ar.zero()
@@ -462,6 +463,7 @@ def main():
         for p_, v_ in zip(params, ar.views):
             p_.grad = v_
         r.after_field_bwd = None        # reduce_and_step launches every bucket itself
+        r.after_grid_levels = None
         opt = FusedAdam(params, lr=1e-2, eps=1e-15)   # train_ml.py:143 (apex defaults)
         tgt = torch.rand(B, 3, generator=torch.Generator().manual_seed(7 + rank)).to(dev)
 

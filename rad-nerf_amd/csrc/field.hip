@@ -395,15 +395,18 @@ struct FxGrad {
 __device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? v - W2_RING : v; }
 
 // issue up to 32 records of stream s (wave-uniform) as one atomic instruction
-// (FULL: exactly 32, every lane issues: no exec-mask region)
-template <int GM, bool FULL = false>
+// (FULL: exactly 32, every lane issues: no exec-mask region).  ODD = s & 1, a
+// template argument: the stream's level (even streams level wid, odd 15 -
+// wid) selects its scale, page and statistics registers at compile time (as a
+// runtime select the compiler emitted both paths with ~12 register copies of
+// the 64-bit sums per issue)
+template <int GM, bool ODD, bool FULL = false>
 __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
     const int lane = rn_lane();
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
-    // the stream's level: even streams level wid, odd 15 - wid (scalar)
-    const bool odd = s & 1;
+    constexpr bool odd = ODD;
     // the level's scale as float bits selected on the scalar unit (gfx9 has
     // no scalar float compare: a float test here became a VALU compare + vcc
     // branch per issue)
@@ -524,17 +527,24 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
         const uint32_t pend = W.pend;
         // lane 0 of each stream's quad (a plain compare's ballot: no
         // bool -> mask round trip)
-        uint64_t m = __builtin_amdgcn_ballot_w64(pend >= need) & 0x1111111111111111ull;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(pend >= need) & 0x1111111111111111ull;
         if (!m) break;
-        while (m) {
-            const int s = __builtin_ctzll(m) >> 2;
-            const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
-            if (min_cnt >= 32u)     // threshold drain (constant after inlining): p >= 32
-                walk2_issue<GM, true>(W, s, 32u, grad_rs, G, dbg);
-            else
-                walk2_issue<GM>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
-            m &= m - 1;
-        }
+        // even streams (lanes 8k), then odd ones (8k + 4): each loop's level
+        // is known at compile time (walk2_issue<ODD>)
+        auto run = [&](uint64_t mm, auto odd_c) {
+            constexpr bool O = decltype(odd_c)::value;
+            while (mm) {
+                const int s = __builtin_ctzll(mm) >> 2;
+                const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
+                if (min_cnt >= 32u)     // threshold drain (constant after inlining): p >= 32
+                    walk2_issue<GM, O, true>(W, s, 32u, grad_rs, G, dbg);
+                else
+                    walk2_issue<GM, O>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
+                mm &= mm - 1;
+            }
+        };
+        run(m & 0x0101010101010101ull, std::integral_constant<bool, false>{});
+        run(m & 0x1010101010101010ull, std::integral_constant<bool, true>{});
         if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
     }
 }

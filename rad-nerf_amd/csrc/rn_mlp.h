@@ -64,14 +64,37 @@ __device__ __forceinline__ void rn_acc_to_frags(const f32x16& acc, half8& f0, ha
     }
 }
 
-// backward ReLU: keep gradient where the forward activation (f16) was > 0
+// backward ReLU: keep gradient where the forward activation (f16) was > 0.
+// The activations are ReLU outputs (>= 0, or -0), so "> 0" is "not +-0": per
+// f16 pair, (m & 0x7fff) -> min(., 1) -> 0 - . gives a 0 / 0xffff mask that
+// is ANDed onto the RNE-converted pair (packed u16 ops, 2 elements each; the
+// per-element compare + select + repack took ~3.5 VALU per element plus
+// hazard nops).  Bit-identical to the select form (masked lanes are +0).
+__device__ __forceinline__ uint32_t rn_relu_mask2(uint32_t mbits) {
+    // (written as u16x2 min / subtract, the compiler turned it back into two
+    // compares + selects + a permute per pair: packed ops are spelled out)
+    uint32_t t, r;
+    // (op_sel_hi:[1,0]: the inline constant 1 is a 32-bit 0x00000001, so the
+    // high lane reads its low half too)
+    asm("v_pk_min_u16 %0, %1, 1 op_sel_hi:[1,0]" : "=v"(t) : "v"(mbits & 0x7fff7fffu));
+    asm("v_pk_sub_u16 %0, 0, %1" : "=v"(r) : "v"(t));
+    return r;
+}
 __device__ __forceinline__ void rn_acc_to_frags_masked(const f32x16& acc, const half8& m0,
                                                        const half8& m1, half8& f0, half8& f1) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4 mb0 = __builtin_bit_cast(u4, m0), mb1 = __builtin_bit_cast(u4, m1);
+    u4 r0, r1;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        f0[j] = (float)m0[j] > 0.f ? (rn_half)acc[j] : (rn_half)0.f;
-        f1[j] = (float)m1[j] > 0.f ? (rn_half)acc[8 + j] : (rn_half)0.f;
+    for (int j = 0; j < 4; ++j) {
+        const h2 a = h2{(rn_half)acc[2 * j], (rn_half)acc[2 * j + 1]};
+        const h2 b = h2{(rn_half)acc[8 + 2 * j], (rn_half)acc[8 + 2 * j + 1]};
+        r0[j] = __builtin_bit_cast(uint32_t, a) & rn_relu_mask2(mb0[j]);
+        r1[j] = __builtin_bit_cast(uint32_t, b) & rn_relu_mask2(mb1[j]);
     }
+    f0 = __builtin_bit_cast(half8, r0);
+    f1 = __builtin_bit_cast(half8, r1);
 }
 
 // cooperative copy of n_bytes (multiple of 16) global -> LDS by a whole block

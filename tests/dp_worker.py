@@ -36,6 +36,76 @@ def step(r, o, d, nz, sd, bg, views):
                gate_grad=views[2])
 
 
+def hooked_split_schedule(rank, dev):
+    """bench.py's N > 1 schedule through the renderer's own hooks, at scale 16
+    (binned fold split into fine / coarse sum launches):
+    the MLP + gate bucket after field_bwd, levels [8, 16) after their sum
+    pass, levels [0, 8) after the backward -- comm-stream launches, forced over
+    gloo.  Each range's local values are copied (main stream) just before its
+    collective starts; the result must equal one plain all-reduce of those
+    local values, bit for bit.  Steps 1-2 set the fixed-point scales; step 3
+    is checked (binned, no redo)."""
+    B, K, scale = 512, 2, 16.0
+    model = MNGP(scale, size=K, seed=5).to(dev)
+    gate = Ray_Gate(K, seed=6).to(dev)
+    bits = S.bitfields(K, model.cascades, p=0.5, seed=7)
+    with torch.no_grad():
+        for i in range(K):
+            getattr(model, f"density_bitfield_{i}").copy_(torch.from_numpy(bits[i]))
+    bg = torch.zeros(3, device=dev)
+    r = FusedMLRenderer(model, gate, B)
+    r.grid_fx = r.grid_bin = True            # (512 x 2 rays: fp32 by the renderer's choice)
+    ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
+    off = model.xyz_encoder.h_offset
+    rg = rdist.step_ranges(ar, off, r.grid_split_level)
+    pending, cut, splits, local = [], [None], [], {}
+
+    def launch(a, b, n):
+        local[(a, b)] = ar.flat[a:b].clone()          # main stream: the local values
+        pending.append(ar.launch_range(a, b, n, stream_ordered=True))
+
+    def mlp_bucket():
+        # (the gate backward ran on the renderer's side stream, as in bench.py)
+        torch.cuda.current_stream(dev).wait_stream(r._side(dev))
+        launch(*rg["rest"], 1)
+
+    def lv(split):
+        a, b = rdist.step_ranges(ar, off, split)["fine"]
+        launch(a, b, 4)
+        cut[0] = a
+        splits.append(split)
+
+    r.after_field_bwd = mlp_bucket
+    r.after_grid_levels = lv
+    o, d, nz, sd = inputs(rank, B, K, scale, dev)
+    for _ in range(3):
+        ar.zero()
+        pending.clear()
+        local.clear()
+        cut[0] = None
+        _, _, _, g_out, _ = r.forward(o, d, d, nz, bg, 1e-4, 1 / 256)
+        r.backward(o, d, d, g_out, bg, *sd, None, 1e-4, grid_grad=ar.views[0],
+                   mlp_grad=ar.views[1], gate_grad=ar.views[2])
+        g0 = ar.param_range(0, 1)[0]
+        if cut[0] is not None and cut[0] > g0:
+            launch(g0, cut[0], 1)
+        for h in pending:
+            ar.finish(h)
+    torch.cuda.synchronize()
+    ref = torch.zeros_like(ar.flat)
+    covered = torch.zeros(ar.flat.numel(), dtype=torch.int32, device=dev)
+    for (a, b), v in local.items():
+        ref[a:b] = v
+        covered[a:b] += 1
+    dist.all_reduce(ref)
+    ref.div_(dist.get_world_size())
+    r.after_field_bwd = r.after_grid_levels = None
+    return {"equal": bool(torch.equal(ar.flat, ref)), "splits": splits,
+            "covered_once": bool((covered == 1).all()), "n_ranges": len(local),
+            "redo": int(r.ws._fx[3][0]), "pages": int(r.ws._bin["ctl"][0]),
+            "finite": bool(torch.isfinite(ar.flat).all()), "nonzero": bool(ar.flat.abs().max() > 0)}
+
+
 def main(out_path):
     rank, _, world = rdist.init(backend="gloo")
     torch.cuda.set_device(0)
@@ -78,6 +148,7 @@ def main(out_path):
     torch.cuda.synchronize()
     staged_equal = bool(torch.equal(staged, ar.flat))
     ar.flat.copy_(result)
+    hooked = hooked_split_schedule(rank, dev)
     if rank == 0:
         ref = rdist.GradAllReduce(params, dev)      # not reduced: a local buffer
         ref.zero()
@@ -89,7 +160,8 @@ def main(out_path):
                "mlp_rel": rel(ar.views[1], ref.views[1]),
                "gate_rel": rel(ar.views[2], ref.views[2]),
                "staged_equal": staged_equal, "staged_stats": stats,
-               "staged_cuda": all(h["cuda"] for h in hs), "n_flat": ar.flat.numel()}
+               "staged_cuda": all(h["cuda"] for h in hs), "n_flat": ar.flat.numel(),
+               "hooked": hooked}
         with open(out_path, "w") as f:
             json.dump(res, f)
     dist.barrier()

@@ -54,6 +54,12 @@ def test_data_parallel_two_ranks_one_gpu(tmp_path):
     assert res["grid_rel"] <= 1e-4 and res["mlp_rel"] <= 1e-4 and res["gate_rel"] <= 1e-4, res
     # the comm-stream staged all-reduce (bench.py's N > 1 form over RCCL), forced over gloo
     assert res["staged_cuda"] and res["staged_equal"], res
+    # the renderer's hooks at scale 16: MLP + gate, fine levels after their
+    # sum pass, coarse levels after the backward -- the plain mean, bit for bit
+    hk = res["hooked"]
+    assert hk["equal"] and hk["finite"] and hk["nonzero"], hk
+    assert hk["covered_once"] and hk["n_ranges"] == 3, hk
+    assert hk["splits"] == [8, 8, 8] and hk["redo"] == 0 and hk["pages"] > 0, hk
     st = res["staged_stats"]
     assert st["buckets_per_step"] == 5 and st["allreduce_ms"] > 0, st
     assert st["bytes_per_rank"] == 4 * res["n_flat"], st
