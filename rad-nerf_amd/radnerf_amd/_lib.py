@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("RADNERF_LIB", os.path.join(_HERE, "librn.so"))
 # sources built with -DRN_ABLATION, where rn_set_debug_flags switches kernel
 # parts off and selects variant kernels (csrc/rn_common.h RN_ABL).  librn.so
 # ignores the switches and holds one code path per kernel.
-ABLATION_LIB_PATH = os.path.join(_HERE, "librn_abl.so")
+ABLATION_LIB_PATH = os.environ.get("RADNERF_ABL_LIB", os.path.join(_HERE, "librn_abl.so"))
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32

@@ -127,7 +127,10 @@ def main():
                                       [round(float(x), 4) for x in
                                        (np.median(np.array(v)[:, 4:], 0) /
                                         max(1.0, float(np.median(np.array(v)[:, 0]))))]))
-                          for f, v in phases.items()}}
+                          for f, v in phases.items()},
+           # the same summed wave cycles, absolute (medians over rounds)
+           "phase_cycles": {f: [float(x) for x in np.median(np.array(v), 0)]
+                            for f, v in phases.items()}}
     print(json.dumps(out))
 
 
