@@ -304,6 +304,11 @@ struct Walk2 {
     // (fx_weight): two entries that wrap in opposite directions cancel in
     // the plain sum but not in this one
     uint64_t swA, swB;
+    // ... accumulated as unsigned products q_u32 * w (one 32x32 -> 64 mad per
+    // record); the sum of w over the negative records, times 2^32, is taken
+    // off at the end of the walk (walk2_end): (int64) q * w = q_u32 * w -
+    // [q < 0] w 2^32 mod 2^64
+    uint32_t cA, cB;
     // binned mode (GM 4): each level's open page in the pool and its fill,
     // and the levels' first entries (wave-uniform)
     uint32_t pgA, pgB, nA, nB, loffA, loffB;
@@ -317,6 +322,7 @@ __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     // after its last issue, so they are not reset here)
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
     W.offA = W.offB = 0;
+    W.cA = W.cB = 0u;
 }
 
 // Exact integer accumulation of the grid gradient (IG mode).  Each record
@@ -380,7 +386,14 @@ static_assert(sizeof(FxStats) == RN_FX_STATS_BYTES, "FxStats layout (include/rad
 // position-weighted checksums: a bijection of i mod 2^32 (odd multiplier), so
 // wraps of +-2^32 on two different elements a, b cancel only if w_a == w_b
 // (mod 2^32), i.e. never
-__host__ __device__ __forceinline__ uint32_t fx_weight(uint32_t i) { return i * 2654435761u; }
+// A 24-bit multiply (full rate; a 32-bit one is quarter rate on the walk's
+// issue path): i < 2^24 (rn_field_bwd_merged refuses fixed point for larger
+// tables) and the odd multiplier keep w injective, since (a - b) * M = 0
+// mod 2^32 only for a = b
+#define FX_WEIGHT_M 0x9E3779u
+__host__ __device__ __forceinline__ uint32_t fx_weight(uint32_t i) {
+    return (i & 0xffffffu) * FX_WEIGHT_M;          // = __umul24(i, M): low 32 bits
+}
 
 struct FxGrad {
     int32_t* acc;              // int32 [entries][2]
@@ -472,17 +485,27 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                 if (rn_dbg(dbg) & 8) *dst = word;                // (timing only: plain stores)
                 else __builtin_nontemporal_store(word, dst);
             }
-        } else if (GM == 2 && fx_lvl) {
+        } else if (GM == 2) {
             const uint32_t ab = v & 0x7fffffffu;          // |v| bits: NaN / inf order last
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             // 2^e_l is a power of two: v * sc is exact; v_cvt_i32_f32 saturates
             // out-of-range values (NaN -> 0): such records are caught by vmax
-            // and the step is redone in fp32
+            // and the step is redone in fp32.  An fp32 level's scale is +-0, so
+            // its q is 0 and the sums below do not move: only the atomic
+            // differs, and the statistics stay out of the branch (as a branch
+            // the compiler copied the 64-bit sums at every issue)
             int q;
             asm("v_cvt_i32_f32 %0, %1" : "=v"(q) : "v"(rintf(__uint_as_float(v) * sc_s)));
-            (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
-            const uint64_t wq = (uint64_t)((int64_t)q * (int64_t)fx_weight(off >> 2));
-            if (odd) { W.sqB += (int64_t)q; W.swB += wq; } else { W.sqA += (int64_t)q; W.swA += wq; }
+            if (fx_lvl)
+                (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(q, G.fx, (int)off, 0, 0);
+            else
+                __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
+                                                            (int)off, 0, 0);
+            const uint32_t w = fx_weight(off >> 2);
+            const uint32_t neg = w & (uint32_t)(q >> 31);
+            const uint64_t qw = (uint64_t)(uint32_t)q * (uint64_t)w;
+            if (odd) { W.sqB += (int64_t)q; W.swB += qw; W.cB += neg; }
+            else { W.sqA += (int64_t)q; W.swA += qw; W.cA += neg; }
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -675,6 +698,8 @@ __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
     walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, lc.off);
     walk2_drain<GM>(W, 0u, grad_rs, G, dbg);
     if (GM == 1) walk2_settle(W, G);
+    W.swA -= (uint64_t)W.cA << 32;          // the negative records' 2^32 w terms
+    W.swB -= (uint64_t)W.cB << 32;
     walk2_begin(W, W.ring);
 }
 
@@ -2359,6 +2384,10 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  perm && chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && dL_dsigma && dL_drgb && grid_grad &&
                  dw && scratch && park, "null pointer");
+    // fixed point: the wrap checksum's element weights are 24-bit (fx_weight)
+    RN_CHECK_ARG(fx_mode != 2 ||
+                 2ull * ((uint64_t)level_offset[RN_L - 1] + level_hsize[RN_L - 1]) <= (1ull << 24),
+                 "fixed-point mode: the grid has more than 2^24 gradient elements");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.dbg = rn_dbg(g_field_dbg);

@@ -70,7 +70,9 @@ extern "C" {
 // rn_grid_bin / rn_grid_sum / rn_grid_binned_fold added.  3 (round 4) the
 // fx_stats block grew to 640 B (position-weighted sums wq / we).  4 (round 5)
 // binned records are e5m17 (rn_grid_record_encode / _decode), the GbCtl block
-// carries a fault word, rn_grid_bin_layout fills 8 values.
+// carries a fault word, rn_grid_bin_layout fills 8 values.  5 (round 5) the
+// wrap checksums wq / we weight element i by ((i mod 2^24) * 0x9E3779) mod
+// 2^32 (a 24-bit multiply), fx_mode 2 refuses grids over 2^24 elements.
 int rn_version(void) { return RN_ABI_VERSION; }
 
 const char* rn_last_error(void) { return g_err; }

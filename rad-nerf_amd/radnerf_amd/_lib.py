@@ -94,7 +94,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 _lib = None
 
 
