@@ -108,13 +108,14 @@ class GradAllReduce:
         last = len(sizes) if last is None else last
         return sum(sizes[:first]), sum(sizes[:last])
 
-    def launch_range(self, a, b, n_buckets=1, stream_ordered=None):
+    def launch_range(self, a, b, n_buckets=1, stream_ordered=None, force=False):
         """Start SUM all-reduces of flat[a:b] in n_buckets pieces as soon as the
         compute stream has produced them: on a comm stream that waits for the
         compute stream, bracketed by events there (CUDA), so the collectives
         overlap whatever the compute stream does next.  Returns a handle for
-        finish(); a no-op with one rank."""
-        if not (dist.is_initialized() and dist.get_world_size() > 1):
+        finish(); a no-op with one rank unless `force` (a one-rank RCCL group:
+        the only RCCL group a one-GPU box can build, tests/rccl_worker.py)."""
+        if not (dist.is_initialized() and (dist.get_world_size() > 1 or force)):
             return None
         n = b - a
         n_buckets = max(1, min(int(n_buckets), max(1, n // 64)))

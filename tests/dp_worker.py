@@ -36,7 +36,7 @@ def step(r, o, d, nz, sd, bg, views):
                gate_grad=views[2])
 
 
-def hooked_split_schedule(rank, dev):
+def hooked_split_schedule(rank, dev, stream_ordered=True, force=False):
     """bench.py's N > 1 schedule through the renderer's own hooks, at scale 16
     (binned fold split into fine / coarse sum launches):
     the MLP + gate bucket after field_bwd, levels [8, 16) after their sum
@@ -44,7 +44,9 @@ def hooked_split_schedule(rank, dev):
     gloo.  Each range's local values are copied (main stream) just before its
     collective starts; the result must equal one plain all-reduce of those
     local values, bit for bit.  Steps 1-2 set the fixed-point scales; step 3
-    is checked (binned, no redo)."""
+    is checked (binned, no redo).  (tests/rccl_worker.py runs the same over a
+    one-rank RCCL group: stream_ordered=None picks the backend's form, force
+    issues the collectives with one rank.)"""
     B, K, scale = 512, 2, 16.0
     model = MNGP(scale, size=K, seed=5).to(dev)
     gate = Ray_Gate(K, seed=6).to(dev)
@@ -62,7 +64,7 @@ def hooked_split_schedule(rank, dev):
 
     def launch(a, b, n):
         local[(a, b)] = ar.flat[a:b].clone()          # main stream: the local values
-        pending.append(ar.launch_range(a, b, n, stream_ordered=True))
+        pending.append(ar.launch_range(a, b, n, stream_ordered=stream_ordered, force=force))
 
     def mlp_bucket():
         # (the gate backward ran on the renderer's side stream, as in bench.py)
@@ -101,6 +103,7 @@ def hooked_split_schedule(rank, dev):
     ref.div_(dist.get_world_size())
     r.after_field_bwd = r.after_grid_levels = None
     return {"equal": bool(torch.equal(ar.flat, ref)), "splits": splits,
+            "cuda": [bool(h["cuda"]) for h in ar.timed[-len(local):]] if ar.timed else [],
             "covered_once": bool((covered == 1).all()), "n_ranges": len(local),
             "redo": int(r.ws._fx[3][0]), "pages": int(r.ws._bin["ctl"][0]),
             "finite": bool(torch.isfinite(ar.flat).all()), "nonzero": bool(ar.flat.abs().max() > 0)}

@@ -6,8 +6,11 @@ as they issue them: the bucketed asynchronous all-reduce of
 dist.GradAllReduce (slices of the flat buffer, work.wait() then the division
 on the compute stream), the pinned layout's all_gather_into_tensor
 (pinned.all_gather_rows), bench.py's all_gather_object (ranks_seen), its
-float64 MAX all-reduce of the elapsed time, and barrier; rank 0 writes what
-it saw."""
+float64 MAX all-reduce of the elapsed time, and barrier; then bench.py's
+N > 1 schedule through the renderer's hooks (dp_worker.hooked_split_schedule
+at scale 16: the MLP + gate bucket after field_bwd, the fine levels after
+their sum pass, the coarse ones after the backward), in the comm-stream form
+RCCL takes, forced with one rank; rank 0 writes what it saw."""
 import json
 import os
 import sys
@@ -19,6 +22,9 @@ import torch.distributed as dist  # noqa: E402
 
 from radnerf_amd import dist as rdist  # noqa: E402
 from radnerf_amd.pinned import all_gather_rows  # noqa: E402
+
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from dp_worker import hooked_split_schedule  # noqa: E402
 
 
 def main(out_path):
@@ -47,6 +53,7 @@ def main(out_path):
     t = torch.tensor(1.25, device=dev, dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     res["max_f64"] = float(t)
+    res["hooked"] = hooked_split_schedule(0, dev, stream_ordered=None, force=True)
     dist.barrier()
     torch.cuda.synchronize()
     with open(out_path, "w") as f:

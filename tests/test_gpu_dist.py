@@ -112,7 +112,9 @@ def test_rccl_calls_world1(tmp_path):
     """Every collective of the multi-GPU paths, issued through RCCL as they
     issue it, in a one-rank RCCL group on GPU 0 (tests/rccl_worker.py): the
     calls are legal for the backend (async bucket slices, tensor and object
-    all-gathers, f64 MAX, barrier) and leave the data as expected."""
+    all-gathers, f64 MAX, barrier) and leave the data as expected; and the
+    renderer's hook schedule (bench.py's early MLP + gate bucket and the split
+    grid ranges) runs on RCCL's comm-stream path."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     out = tmp_path / "rccl.json"
@@ -127,3 +129,9 @@ def test_rccl_calls_world1(tmp_path):
     assert res["all_gather_rows_equal"]
     assert res["all_gather_object"] == [{"rank": 0, "device": 0}]
     assert res["max_f64"] == 1.25
+    # the renderer's hook schedule over RCCL (comm stream, events): every range
+    # once, the sum over one rank = the local values, bit for bit
+    hk = res["hooked"]
+    assert hk["equal"] and hk["finite"] and hk["nonzero"], hk
+    assert hk["covered_once"] and hk["n_ranges"] == 3 and all(hk["cuda"]), hk
+    assert hk["splits"] == [8, 8, 8] and hk["redo"] == 0 and hk["pages"] > 0, hk
