@@ -130,6 +130,9 @@ def parse():
     ap.add_argument("--max-chunk", type=int, default=None,
                     help="merged backward: largest chunk of merged samples per queue grab "
                          "(default: the renderer's, by rays x sub-NeRFs)")
+    ap.add_argument("--balance-chunks", type=int, default=None,
+                    help="merged backward: 1 = big chunks a multiple of the persistent "
+                         "blocks in number (the renderer's default), 0 = max_chunk each")
     ap.add_argument("--head-chunk", type=int, default=0,
                     help="merged passes: first chunk per block (0 = none)")
     ap.add_argument("--pinned", action="store_true",
@@ -296,6 +299,8 @@ def main():
     if args.max_chunk:
         r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk
+    if args.balance_chunks is not None:
+        r.balance_chunks = bool(args.balance_chunks)
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
 

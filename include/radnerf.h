@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 5   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 6   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -204,11 +204,15 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * rn_bwd_plan builds the merged order (mstart [n_rays + 1] i32, perm [total]
  * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: head_chunks
  * chunks of head_size merged samples (one per block, so the first scatter
- * starts early), then max_chunk up to 7/8 of the work, then min_chunk;
+ * starts early), then big chunks up to 7/8 of the work, then min_chunk;
+ * the big chunks are max_chunk merged samples, or with balance_blocks > 0 a
+ * multiple of balance_blocks in number, each of at most max_chunk (every
+ * persistent block takes the same number of them);
  * queue [3] i32 = bwd ticket, chunk count, fwd ticket; chunk_desc
  * [cap_chunks][20] i32 = first ray, end ray, 2 pad, first sample [8], count [8]
  * per model, read by the merged kernels with one 80-B load per ticket).  cap_chunks must bound the chunk
- * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2.
+ * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2
+ * (+ balance_blocks when balancing).
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
  * stages 80-B rows in its scratch slice (scratch: blocks x scratch_rows x 20
  * f32, scratch_rows >= max_chunk + n_models * max_samples) and parks per-model
@@ -219,8 +223,8 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
 int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
-                int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
-                int32_t* chunk_desc, int32_t* queue, void* stream);
+                int32_t balance_blocks, int32_t cap_chunks, int32_t* mstart, int32_t* perm,
+                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, void* stream);
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* mstart, const int32_t* perm,

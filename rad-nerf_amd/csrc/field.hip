@@ -2107,13 +2107,19 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
 }
 
 // Chunk schedule of the merged backward over the merged positions [0, total):
-// chunks of max_chunk positions for the first 7/8 of the work, then chunks of
-// min_chunk (a short tail: blocks finish together).  Chunk c holds the rays
-// whose merged start lies in [bound(c), bound(c+1)), so it is whole rays of
-// at most max_chunk + K * max_samples samples (possibly none).
+// big chunks for the first 7/8 of the work, then chunks of min_chunk (a short
+// tail: blocks finish together).  With `blocks` > 0 the big chunks are a
+// multiple of the persistent blocks in number, each <= max_chunk positions
+// (size ceil(main / (blocks m)), m = ceil(main / (blocks max_chunk))): every
+// block takes m of them.  A count just past a multiple (C4 at 2560: 534 big
+// chunks for 256 blocks) left a few blocks one big chunk behind the rest, a
+// tail the min_chunk phase was too small to hide (C4 485 vs 523 M samples/s
+// at 2560 vs 3072).  Chunk c holds the rays whose merged start lies in
+// [bound(c), bound(c+1)), so it is whole rays of at most max_chunk + K *
+// max_samples samples (possibly none).
 struct ChunkPlan {
     int head_n, head, max_chunk, min_chunk, c1, n;
-    __device__ int bound(int c) const {
+    __host__ __device__ int bound(int c) const {
         const int H = head_n * head;
         if (c < head_n) return c * head;
         if (c <= c1) return H + (c - head_n) * max_chunk;
@@ -2124,14 +2130,20 @@ struct ChunkPlan {
 // head_n chunks of `head` samples first (one per block: the scatter, and so the
 // atomics, start after a short MLP phase instead of a full chunk's), then
 // max_chunk up to 7/8 of the work, then min_chunk
-__device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head, int max_chunk,
-                                                int min_chunk) {
+__host__ __device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head,
+                                                         int max_chunk, int min_chunk, int blocks) {
     ChunkPlan p;
     p.head = head; p.max_chunk = max_chunk; p.min_chunk = min_chunk;
     const int main_end = total - total / 8;
     p.head_n = head > 0 ? min(head_n, main_end / head) : 0;
     const int H = p.head_n * head;
-    p.c1 = p.head_n + (main_end > H ? (main_end - H) / max_chunk : 0);
+    if (blocks > 0 && main_end > H) {
+        const int64_t main = main_end - H, per = (int64_t)blocks * max_chunk;
+        const int64_t m = (main + per - 1) / per;
+        const int64_t sz = (main + (int64_t)blocks * m - 1) / ((int64_t)blocks * m);
+        p.max_chunk = (int)(sz < min_chunk ? min_chunk : (sz > max_chunk ? max_chunk : sz));
+    }
+    p.c1 = p.head_n + (main_end > H ? (main_end - H) / p.max_chunk : 0);
     const int rest = total - p.bound(p.c1);
     p.n = p.c1 + (rest > 0 ? (rest + min_chunk - 1) / min_chunk : 0);
     return p;
@@ -2141,11 +2153,11 @@ __global__ void __launch_bounds__(256)
 k_bwd_chunks(int B, int K, const int32_t* __restrict__ mstart,
              const int32_t* __restrict__ offsets, const int32_t* __restrict__ seg_base,
              const int32_t* __restrict__ seg_count, int head_n, int head, int max_chunk,
-             int min_chunk, int cap_chunks, int32_t* __restrict__ chunk_first,
+             int min_chunk, int blocks, int cap_chunks, int32_t* __restrict__ chunk_first,
              int32_t* __restrict__ desc, int32_t* __restrict__ queue) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     const int total = mstart[B];
-    const ChunkPlan p = chunk_plan(total, head_n, head, max_chunk, min_chunk);
+    const ChunkPlan p = chunk_plan(total, head_n, head, max_chunk, min_chunk, blocks);
     const int n = min(p.n, cap_chunks);
     if (c == 0) { queue[0] = 0; queue[1] = n; queue[2] = 0; }
     if (c > n) return;
@@ -2324,11 +2336,12 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
 int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* seg_base,
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
-                int32_t cap_chunks, int32_t* mstart, int32_t* perm, int32_t* chunk_first,
-                int32_t* chunk_desc, int32_t* queue, void* stream) {
+                int32_t balance_blocks, int32_t cap_chunks, int32_t* mstart, int32_t* perm,
+                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX, "bad sizes");
     RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1 && head_chunks >= 0 &&
-                 head_size >= 0 && head_size <= max_chunk, "bad chunk sizes");
+                 head_size >= 0 && head_size <= max_chunk && balance_blocks >= 0,
+                 "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
                  chunk_first && chunk_desc && queue, "null pointer");
     if (n_models > 2)
@@ -2340,7 +2353,7 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, mstart, offsets, seg_base, seg_count, head_chunks, head_size,
-        max_chunk, min_chunk, cap_chunks, chunk_first, chunk_desc, queue);
+        max_chunk, min_chunk, balance_blocks, cap_chunks, chunk_first, chunk_desc, queue);
     RN_CHECK_LAUNCH();
     return 0;
 }

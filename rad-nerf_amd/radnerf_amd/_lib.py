@@ -59,7 +59,7 @@ SIGNATURES = {
     "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, I32, P],
     "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                      I32, P],
-    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
+    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
                             P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P, P, P,
                             P, I32, P, P, P, I32, P],
@@ -94,7 +94,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 _lib = None
 
 

@@ -73,9 +73,10 @@ class Workspace:
         self._chunks = None
         self.generation = 0         # forwards run through this workspace (_MLRenderFn)
 
-    def chunk_list(self, max_chunk, min_chunk, head_chunks=0):
+    def chunk_list(self, max_chunk, min_chunk, head_chunks=0, balance_blocks=0):
         """rn_bwd_plan's chunk list, sized for the workspace capacity."""
-        cap = head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2
+        cap = (head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2 +
+               balance_blocks)
         if self._chunks is None or self._chunks.numel() < cap + 1:
             self._chunks = torch.empty(cap + 1, device=self.device, dtype=torch.int32)
             self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
@@ -220,8 +221,16 @@ class FusedMLRenderer:
         # scale 16 (C5 per GPU) 1024 12.36, 2048 12.23 ms; K = 4 at scale 16
         # (C4 per GPU) keeps 1024 (3.82 vs 3.92 at 1536); K = 1 (C2) 512-1024
         # within 0.6 % (tools/step_variants.py, profiles/r02/step_variants_fx_chunk.json)
+        # Round 5, with the big chunks balanced over the blocks (balance_chunks
+        # below): longer chunks pay at K >= 4 (fewer model switches -- park /
+        # unpark dW, reload weights -- and ring drains per sample): C5 per GPU
+        # 2048 645, 4096 664, 6144 670, 8192 671-675; C4 1024 512, 2048 533,
+        # 3072 535, 4096 537, 6144 422; C3 1024 1136, 1536 1158, 2048 1148
+        # (profiles/r05/chunk3/)
         if model.size >= 8 and rk > 4096:
-            self.max_chunk = 2048
+            self.max_chunk = 8192
+        elif model.size >= 4 and rk > 4096 and float(model.scale) > 0.5:
+            self.max_chunk = 4096
         elif model.size >= 2 and rk > 4096 and float(model.scale) <= 0.5:
             self.max_chunk = 1536
         # exact integer accumulation of the grid gradient (rn_seed_scale +
@@ -261,6 +270,9 @@ class FusedMLRenderer:
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
         self.head_chunk = 0
+        # big chunks a multiple of the persistent blocks in number (rn_bwd_plan
+        # balance_blocks): every block takes the same number of them
+        self.balance_chunks = True
         # gate backward on this process (pinned.PinnedMLRenderer: rank 0 only),
         # and where: "field" side stream beside field_bwd, "early" side stream
         # beside composite_bw, "main" in line before field_bwd
@@ -414,13 +426,14 @@ class FusedMLRenderer:
         self._min_chunk = min(self.min_chunk, self.max_chunk)
         head_n = self.merged_blocks if self.head_chunk else 0
         head = min(self.head_chunk, self.max_chunk)
-        self._cap_chunks, self._chunks = w.chunk_list(self.max_chunk, self._min_chunk, head_n)
+        bal = self.merged_blocks if self.balance_chunks else 0
+        self._cap_chunks, self._chunks = w.chunk_list(self.max_chunk, self._min_chunk, head_n, bal)
         self._ev("bwd_plan", L.bwd_plan, w.counts.data_ptr(), w.offsets.data_ptr(),
                  w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, w.K,
-                 head_n, head, self.max_chunk, self._min_chunk, self._cap_chunks,
+                 head_n, head, self.max_chunk, self._min_chunk, bal, self._cap_chunks,
                  w.mstart.data_ptr(), w.perm.data_ptr(), self._chunks.data_ptr(),
                  w._chunk_desc.data_ptr(), w.queue.data_ptr(), st)
-        self._plan_key = (self.max_chunk, self._min_chunk, head_n, head)
+        self._plan_key = (self.max_chunk, self._min_chunk, head_n, head, bal)
 
     def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
         m, w, L = self.model, self.ws, lib()
@@ -454,7 +467,8 @@ class FusedMLRenderer:
             if getattr(self, "_plan_key", None) != (
                     self.max_chunk, min(self.min_chunk, self.max_chunk),
                     self.merged_blocks if self.head_chunk else 0,
-                    min(self.head_chunk, self.max_chunk)):
+                    min(self.head_chunk, self.max_chunk),
+                    self.merged_blocks if self.balance_chunks else 0):
                 self._plan(st)      # chunk sizes changed since the forward
             chunks = self._chunks
             ig = (None, None, None)

@@ -348,6 +348,66 @@ def test_merged_backward_chunking(cuda):
             assert rel <= (FX_LEVEL_TOL if i == 0 else 1e-5), rel
 
 
+def _chunk_bounds(total, head_n, head, max_chunk, min_chunk, blocks):
+    """host restatement of field.hip chunk_plan: the merged-position bound of
+    every chunk (head chunks, big chunks over 7/8 of the work -- with blocks >
+    0 a multiple of blocks in number, each <= max_chunk -- then min_chunk)"""
+    main_end = total - total // 8
+    head_n = min(head_n, main_end // head) if head > 0 else 0
+    H = head_n * head
+    big, mm = max_chunk, 0
+    if blocks > 0 and main_end > H:
+        per = blocks * max_chunk
+        mm = -(-(main_end - H) // per)
+        big = min(max(-(-(main_end - H) // (blocks * mm)), min_chunk), max_chunk)
+    c1 = head_n + ((main_end - H) // big if main_end > H else 0)
+
+    def bound(c):
+        if c < head_n:
+            return c * head
+        if c <= c1:
+            return H + (c - head_n) * big
+        return H + (c1 - head_n) * big + (c - c1) * min_chunk
+    rest = total - bound(c1)
+    n = c1 + (-(-rest // min_chunk) if rest > 0 else 0)
+    return [bound(c) for c in range(n)], c1 - head_n, big, mm
+
+
+@pytest.mark.parametrize("B,K,scale,mc,bal", [(2048, 2, 0.5, 1536, 256), (1024, 4, 16.0, 4096, 256),
+                                              (1024, 8, 16.0, 8192, 256), (2048, 2, 0.5, 1536, 0),
+                                              (512, 4, 16.0, 2560, 37)])
+def test_chunk_schedule(cuda, B, K, scale, mc, bal):
+    """rn_bwd_plan's chunk list against the host restatement of its schedule:
+    every chunk starts at the first ray whose merged start reaches its bound,
+    the count is the plan's; balanced (balance_blocks > 0), no block has more
+    big chunks to take than the others (C4 at 2560 left a few blocks one big
+    chunk behind the rest)."""
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    esf = 1.0 / 256 if scale > 0.5 else 0.0
+    r = get_renderer(m, g, B)
+    r.max_chunk, r.balance_chunks = mc, bal > 0
+    if bal:
+        r.merged_blocks = bal
+    _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
+    w = r.ws
+    torch.cuda.synchronize()
+    ms = w.mstart[:B + 1].cpu().numpy().astype(np.int64)
+    total = int(ms[B])
+    bounds, n_big, big, per_block = _chunk_bounds(total, 0, 0, mc, min(r.min_chunk, mc), bal)
+    n = int(w.queue[1])
+    assert n == len(bounds)
+    first = r._chunks[:n + 1].cpu().numpy()
+    assert np.array_equal(first[:n], np.searchsorted(ms[:B], np.array(bounds), side="left"))
+    assert first[n] == B
+    if bal and n_big and big > r.min_chunk:
+        # at most per_block big chunks for every block, and nearly all take
+        # that many (floor division leaves at most a few a chunk short)
+        assert bal * (per_block - 1) < n_big <= bal * per_block and big <= mc, (n_big, big)
+    r.max_chunk, r.merged_blocks, r.balance_chunks = mc, 256, True
+    assert all(torch.isfinite(x).all() for x in gr)
+
+
 @pytest.mark.parametrize("B,K,scale", [(4096, 2, 0.5), (1024, 4, 16.0), (512, 1, 0.5),
                                      (768, 8, 16.0), (512, 5, 0.5)])
 def test_merged_forward_matches_per_model(cuda, B, K, scale):
