@@ -130,6 +130,14 @@ def parse():
     ap.add_argument("--max-chunk", type=int, default=None,
                     help="merged backward: largest chunk of merged samples per queue grab "
                          "(default: the renderer's, by rays x sub-NeRFs)")
+    ap.add_argument("--enc-blocks", type=int, default=None,
+                    help="level-partitioned forward: encode workgroups (a multiple of 8; "
+                         "default: the renderer's, 4096)")
+    ap.add_argument("--mlp-blocks", type=int, default=None,
+                    help="level-partitioned forward: MLP-tile workgroups (default 256)")
+    ap.add_argument("--min-chunk", type=int, default=None,
+                    help="merged backward: chunk of the last 1/8 of the work (default: the "
+                         "renderer's, 512)")
     ap.add_argument("--balance-chunks", type=int, default=None,
                     help="merged backward: 1 = big chunks a multiple of the persistent "
                          "blocks in number (the renderer's default), 0 = max_chunk each")
@@ -299,6 +307,12 @@ def main():
     if args.max_chunk:
         r.max_chunk = args.max_chunk
     r.head_chunk = args.head_chunk
+    if args.min_chunk:
+        r.min_chunk = args.min_chunk
+    if args.enc_blocks:
+        r.level_enc_blocks = args.enc_blocks
+    if args.mlp_blocks:
+        r.level_mlp_blocks = args.mlp_blocks
     if args.balance_chunks is not None:
         r.balance_chunks = bool(args.balance_chunks)
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
