@@ -474,11 +474,15 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             // vmax flags the step for the fp32 redo
             const int q = (int)gb_encode(__uint_as_float(v) * sc_s);
             const int qp = __builtin_amdgcn_mov_dpp(q, 0xb1, 0xf, 0xf, true);   // partner lane ^ 1
-            const uint32_t idx = (base[rec] >> 3) - (odd ? W.loffB : W.loffA);
-            const uint32_t q0 = (uint32_t)((lane & 1) ? qp : q), q1 = (uint32_t)((lane & 1) ? q : qp);
-            const uint32_t word = (lane & 1)
-                ? ((q0 >> 12) & 0x3ffu) | (q1 << 10)
-                : (idx & ((1u << GB_IDX_BITS) - 1u)) | (q0 << 20);
+            // both words on every lane, then a select: with the index read
+            // only on the even lanes the compiler branched on lane & 1 (an
+            // exec-mask if / else per issue)
+            const uint32_t idx = (off >> 3) - (odd ? W.loffB : W.loffA);
+            const bool hi_lane = lane & 1;
+            const uint32_t q0 = (uint32_t)(hi_lane ? qp : q), q1 = (uint32_t)(hi_lane ? q : qp);
+            const uint32_t w_hi = ((q0 >> 12) & 0x3ffu) | (q1 << 10);
+            const uint32_t w_lo = (idx & ((1u << GB_IDX_BITS) - 1u)) | (q0 << 20);
+            const uint32_t word = hi_lane ? w_hi : w_lo;
             const uint32_t pg = odd ? W.pgB : W.pgA, n = odd ? W.nB : W.nA;
             uint32_t* dst = reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane;
             if (pg < G.pool_pages) {

@@ -9,7 +9,7 @@ TAG=${1:-ab}
 OLD=${2:-rad-nerf_amd/radnerf_amd/librn_old.so}
 NEW=rad-nerf_amd/radnerf_amd/librn.so
 Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0 --test-time-rays 0"
-timeout -k 10 400 python -u -m pytest tests/test_gpu_fx.py tests/test_gpu_ml.py -m gpu -q -x -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_fx.py tests/test_gpu_ml.py tests/test_gpu_bin.py -m gpu -q -x -p no:cacheprovider --timeout 200 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc" >> gpurun_out/tests_$TAG.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 for r in 1 2; do
