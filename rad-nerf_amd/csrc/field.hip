@@ -1328,18 +1328,29 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                 const nf4 u = __builtin_bit_cast(nf4, __builtin_amdgcn_raw_buffer_load_b128(
                     rows_rs, rb + 64u, 0, 16));
                 float* dst = sG + j * SG_STRIDE + 16 * half;
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                uint32_t bits = 0u;
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
-                    const h8 v = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(
+                    const u4v raw = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
                         rows_rs, rb + 16u * (2u * half + qq), 0, 16));
+                    const h8 v = __builtin_bit_cast(h8, raw);
+                    bits |= (raw.x | raw.y) | (raw.z | raw.w);
 #pragma unroll
                     for (int e2 = 0; e2 < 8; e2 += 2) {
                         const float a0 = (float)v[e2] * u.w, a1 = (float)v[e2 + 1] * u.w;
                         *reinterpret_cast<float2*>(dst + 8 * qq + e2) = make_float2(a0, a1);
-                        nz |= (a0 != 0.f) | (a1 != 0.f);
                     }
                 }
-                if (half) *reinterpret_cast<nf4*>(sU + j * 4) = u;
+                // any non-zero row value (sign bits masked) with a non-zero
+                // 1/scale: a superset of "some staged product is non-zero"
+                // (only an fp32 underflow of the product differs, and walking
+                // a window of zeros adds nothing); per-element tests of the
+                // products compiled to ~60 VALU per row half
+                nz |= ((bits & 0x7fff7fffu) != 0u) & (u.w != 0.f);
+                // both lanes of the row store the same coordinates (no
+                // lane-parity branch)
+                *reinterpret_cast<nf4*>(sU + j * 4) = u;
             }
           }
             // a window whose rows are all zero (rays past early termination)
