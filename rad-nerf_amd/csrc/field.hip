@@ -1051,6 +1051,7 @@ k_field_bwd(FieldArgs a) {
 // stay in L2 for longer chunks.
 #define MB_ROW 20
 #define MB_WIN 64          // walk window: staged rows per chunk eighth
+#define MB_RI_CAP 4096     // merged positions of a chunk with LDS row indices (else per-row perm reads)
 #define CH_DESC 20         // chunk descriptor ints (80 B, 16-B aligned)
 #define MB_KMAX 8
 
@@ -1108,6 +1109,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     __shared__ DwScale sScale[MB_KMAX];         // per model: scales of its parked dW (0 = none)
     // chunk descriptor: r0, r1, then per model: first sample, count, row offset, segment base
     __shared__ int32_t sCh[2 + 4 * MB_KMAX];
+    // the walk's scratch-row index of each merged position of the chunk
+    __shared__ uint16_t sRowIdx[MB_RI_CAP];
     const int K = m.n_models, B = m.n_rays;
     lv_stage(sT, a.gm);
     if (threadIdx.x < MB_KMAX) sScale[threadIdx.x] = DwScale{0.f, 0.f};
@@ -1288,12 +1291,48 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         if (!do_sc) continue;
 
         // ---- 2. scatter in merged (ray, t) order
+        const int p_base = m.mstart[r0], n_p = m.mstart[r1] - p_base;
+        // scratch row of merged position p: the sample's model k from the
+        // segment bases (branch-free, K <= 8), its row offset in the chunk
+        auto row_of = [&](int p) -> int {
+            const int smp = m.perm[p_base + p];
+            int k = 0;
+#pragma unroll
+            for (int kq = 1; kq < MB_KMAX; ++kq)
+                k = (kq < K && smp >= sCh[2 + 3 * MB_KMAX + kq]) ? kq : k;
+            return sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
+        };
+        // the chunk's row indices in LDS, built once with coalesced perm reads
+        // before the walk issues anything: a window's staging then reads them
+        // from LDS instead of loading perm per row (a global load that waited,
+        // vmcnt in issue order, for every atomic / page store the wave had
+        // issued before it).  A chunk longer than the table reads perm per row.
+        const bool ri_ok = n_p <= MB_RI_CAP;                // block-uniform
+        if (ri_ok) {
+            // all of a thread's perm loads in flight together (a plain loop
+            // waited for each one)
+            constexpr int RI_PER = MB_RI_CAP / (BWD_WAVES * RN_WAVE);
+            int smp[RI_PER];
+#pragma unroll
+            for (int q = 0; q < RI_PER; ++q) {
+                const int p = threadIdx.x + q * BWD_WAVES * RN_WAVE;
+                smp[q] = p < n_p ? m.perm[p_base + p] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < RI_PER; ++q) {
+                const int p = threadIdx.x + q * BWD_WAVES * RN_WAVE;
+                int k = 0;
+#pragma unroll
+                for (int kq = 1; kq < MB_KMAX; ++kq)
+                    k = (kq < K && smp[q] >= sCh[2 + 3 * MB_KMAX + kq]) ? kq : k;
+                if (p < n_p) sRowIdx[p] = (uint16_t)(sCh[2 + 2 * MB_KMAX + k] + (smp[q] - sCh[2 + k]));
+            }
+        }
         __builtin_amdgcn_s_waitcnt(0x0070);     // vmcnt(0): this wave's rows are in L2
         __syncthreads();
         // the chunk's merged order is cut into 8 contiguous eighths, one per
         // stream eighth; each window stages the next 32 rows of every eighth
         // and the walks carry their state across windows (no restart per window)
-        const int p_base = m.mstart[r0], n_p = m.mstart[r1] - p_base;
         const int E = (n_p + 7) >> 3;
         const int elen_lane = max(0, min(E, n_p - (rn_lane() >> 3) * E));   // walk eighth
         Walk2 W;
@@ -1315,10 +1354,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
             const int j = jj;                            // row of the eighth's block
             const int elen = max(0, min(E, n_p - e * E));
             if (w0 + jj < elen) {
-                const int smp = m.perm[p_base + e * E + w0 + jj];
-                int k = 0;
-                for (int kq = 1; kq < K; ++kq) k = smp >= sCh[2 + 3 * MB_KMAX + kq] ? kq : k;
-                const int row_i = sCh[2 + 2 * MB_KMAX + k] + (smp - sCh[2 + k]);
+                const int row_i = ri_ok ? (int)sRowIdx[e * E + w0 + jj] : row_of(e * E + w0 + jj);
                 // rows were written by other waves of this block: read past L1
                 // with sc1 buffer loads (L2-served; the nt loads used before cost
                 // field_bwd 0.09 ms at C3, profiles/r03/rowab_*_r1.json)
@@ -1329,13 +1365,18 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
                     rows_rs, rb + 64u, 0, 16));
                 float* dst = sG + j * SG_STRIDE + 16 * half;
                 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                // both 16-B halves of the row's dL/dE loaded before either is
+                // used (one round trip per row)
+                u4v raw[2];
+#pragma unroll
+                for (int qq = 0; qq < 2; ++qq)
+                    raw[qq] = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
+                        rows_rs, rb + 16u * (2u * half + qq), 0, 16));
                 uint32_t bits = 0u;
 #pragma unroll
                 for (int qq = 0; qq < 2; ++qq) {
-                    const u4v raw = __builtin_bit_cast(u4v, __builtin_amdgcn_raw_buffer_load_b128(
-                        rows_rs, rb + 16u * (2u * half + qq), 0, 16));
-                    const h8 v = __builtin_bit_cast(h8, raw);
-                    bits |= (raw.x | raw.y) | (raw.z | raw.w);
+                    const h8 v = __builtin_bit_cast(h8, raw[qq]);
+                    bits |= (raw[qq].x | raw[qq].y) | (raw[qq].z | raw[qq].w);
 #pragma unroll
                     for (int e2 = 0; e2 < 8; e2 += 2) {
                         const float a0 = (float)v[e2] * u.w, a1 = (float)v[e2 + 1] * u.w;
