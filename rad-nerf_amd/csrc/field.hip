@@ -283,6 +283,15 @@ __device__ __forceinline__ void walk_end(const FieldArgs& a, const LvTab& sT, Sc
 #define W2_RING_WORDS (W2_STREAMS * 3 * W2_RING)   // per wave
 #define W2_NONE 0xffffffffu
 
+// The two levels a wave of the merged backward walks: levels a and 15 - a.
+// Records per sample grow with the level (C3 replay, tools/records_sim.py:
+// 0.20 at level 0 ... 5.58 at level 15), so the pair (0, 15) carries the most
+// and (7, 8) the least.  Waves w and w + 4 of a block share a SIMD: waves
+// 0-3 take the pairs (0, 15) ... (3, 12) and waves 4-7 the pairs (7, 8) ...
+// (4, 11), heaviest with lightest (SIMD issue loads 8.18 / 7.47 / 6.96 / 6.69
+// records per sample instead of 8.88 / 7.70 / 6.73 / 5.99 for a = w).
+__device__ __forceinline__ int w2_level_a(int wid) { return wid < 4 ? wid : 11 - wid; }
+
 struct Walk2 {
     uint32_t* ring;        // this wave's rings: [stream][3][W2_RING] words
     uint32_t head, tail;   // per lane: its stream's ring head / tail, in [0, W2_RING)
@@ -436,7 +445,8 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         if (n + cnt > GB_PAGE) {                         // wave-uniform
             const uint32_t pg = odd ? W.pgB : W.pgA;
             const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-            const uint32_t lvl = odd ? RN_L - 1 - wid : wid;
+            const int la = w2_level_a(wid);
+            const uint32_t lvl = odd ? RN_L - 1 - la : la;
             uint32_t np = 0u;
             if (lane == 0) {
                 if (pg < G.pool_pages) G.page_meta[pg] = lvl | (n << 8);
@@ -612,7 +622,8 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t 
 
 __device__ __forceinline__ LvConst walk2_level(const FieldArgs& a, const LvTab& sT) {
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-    const int l = ((rn_lane() >> 2) & 1) ? (RN_L - 1 - wid) : wid;
+    const int la = w2_level_a(wid);
+    const int l = ((rn_lane() >> 2) & 1) ? (RN_L - 1 - la) : la;
     return lv_const(sT, a.gm, l);
 }
 
@@ -631,7 +642,8 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
     const uint32_t py = lane & 1, pz = (lane >> 1) & 1;
     const LvConst lc = walk2_level(a, sT);
     const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x / RN_WAVE);
-    lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - wid) : wid);
+    const int la = w2_level_a(wid);
+    lds_cf* gcol = sG + 2 * ((stream & 1) ? (RN_L - 1 - la) : la);
     // sG / sU are this lane's eighth's own block of WIN rows (per-lane bases)
     const int s_base = 0;
     (void)eighth;
@@ -1116,6 +1128,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     if (threadIdx.x < MB_KMAX) sScale[threadIdx.x] = DwScale{0.f, 0.f};
 
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
+    const int lvA = w2_level_a(wid);             // this wave's walk levels: lvA, 15 - lvA
     const int lane = rn_lane(), c = lane & 31, h = lane >> 5;
     rn_half* imgY = sImg + wid * 2 * RN_IMG_HALFS;
     rn_half* imgX = imgY + RN_IMG_HALFS;
@@ -1130,8 +1143,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
     // binned mode: this wave's open pages (none yet: the first issue takes one)
     uint32_t pgA = 0xffffffffu, pgB = 0xffffffffu, nA = GB_PAGE, nB = GB_PAGE;
     if (GM >= 2) {
-        fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[wid])));
-        fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - wid])));
+        fxA = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[lvA])));
+        fxB = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(F.scale[RN_L - 1 - lvA])));
     }
     const bool do_sc = !(rn_dbg(dbg) & 4);
     // walk windows of MB_WIN rows per eighth: each window's staging loads
@@ -1340,7 +1353,7 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         W.fxA = fxA; W.fxB = fxB; W.vmA = vmA; W.vmB = vmB; W.sqA = sqA; W.sqB = sqB;
         W.swA = swA; W.swB = swB;
         W.pgA = pgA; W.pgB = pgB; W.nA = nA; W.nB = nB;
-        W.loffA = sT.off[wid]; W.loffB = sT.off[RN_L - 1 - wid];
+        W.loffA = sT.off[lvA]; W.loffB = sT.off[RN_L - 1 - lvA];
         sw_ok = false;                           // the staging overwrites sW
         for (int w0 = 0; w0 < E; w0 += MB_WIN) {
           int nz = 0;
@@ -1419,8 +1432,8 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
         for (int q = 0; q < 8; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
     }
     if (GM == 4 && rn_lane() == 0) {             // close this wave's open pages
-        if (pgA < G.pool_pages) G.page_meta[pgA] = (uint32_t)wid | (nA << 8);
-        if (pgB < G.pool_pages) G.page_meta[pgB] = (uint32_t)(RN_L - 1 - wid) | (nB << 8);
+        if (pgA < G.pool_pages) G.page_meta[pgA] = (uint32_t)lvA | (nA << 8);
+        if (pgB < G.pool_pages) G.page_meta[pgB] = (uint32_t)(RN_L - 1 - lvA) | (nB << 8);
     }
     if (GM == 2 || GM == 4) {                    // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
@@ -1435,14 +1448,14 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
             eB += __shfl_xor(eB, off);
         }
         if (rn_lane() == 0) {
-            if (vmA) atomicMax(F.vmax + wid, vmA);
-            if (vmB) atomicMax(F.vmax + RN_L - 1 - wid, vmB);
-            if (dA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + wid),
+            if (vmA) atomicMax(F.vmax + lvA, vmA);
+            if (vmB) atomicMax(F.vmax + RN_L - 1 - lvA, vmB);
+            if (dA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + lvA),
                                    (unsigned long long)dA);
-            if (dB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + RN_L - 1 - wid),
+            if (dB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.qsum + RN_L - 1 - lvA),
                                    (unsigned long long)dB);
-            if (eA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + wid), eA);
-            if (eB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + RN_L - 1 - wid), eB);
+            if (eA != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + lvA), eA);
+            if (eB != 0) atomicAdd(reinterpret_cast<unsigned long long*>(F.wq + RN_L - 1 - lvA), eB);
         }
     }
     // ---- flush every model's dW (the current one from registers)
