@@ -135,9 +135,6 @@ def parse():
                          "default: the renderer's, 4096)")
     ap.add_argument("--mlp-blocks", type=int, default=None,
                     help="level-partitioned forward: MLP-tile workgroups (default 256)")
-    ap.add_argument("--gate-partials", type=int, default=None,
-                    help="gate backward: 1 = per-block weight-gradient partials summed in "
-                         "block order (the renderer's default), 0 = fp32 atomics per block")
     ap.add_argument("--min-chunk", type=int, default=None,
                     help="merged backward: chunk of the last 1/8 of the work (default: the "
                          "renderer's, 512)")
@@ -312,8 +309,6 @@ def main():
     r.head_chunk = args.head_chunk
     if args.min_chunk:
         r.min_chunk = args.min_chunk
-    if args.gate_partials is not None:
-        r.gate_dw_partials = bool(args.gate_partials)
     if args.enc_blocks:
         r.level_enc_blocks = args.enc_blocks
     if args.mlp_blocks:

@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 7   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 6   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -433,14 +433,11 @@ int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
  * the gate input cat(in0, in1), as tcnn's Network backward provides when the
  * input requires grad (rays_o / rays_d under --optimize_ext,
  * train_ml.py:90-93); needs dinput_frags (4 transposed W0 fragments,
- * radnerf_amd/layout.py gate_dinput_frag_index).  dw_partial (optional,
- * n_blocks x n_params fp32 scratch): each block stores its partial weight
- * gradient there and a second launch adds their sum, in block order, to dw
- * (deterministic); NULL: each block atomically adds its partial to dw.     */
+ * radnerf_amd/layout.py gate_dinput_frag_index).                            */
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays,
                 int32_t n_models, const void* frags, const float* dL_dgate, float* dw,
                 int32_t n_params, const void* dinput_frags, float* dL_dinput,
-                int32_t n_blocks, float* dw_partial, void* stream);
+                int32_t n_blocks, void* stream);
 
 /* ---- field input gradients and density-only evaluation (field_aux.hip) -----
  * rn_field_dinput: dL/dxyz and dL/ddir (fp32, (N, 3) each, written, indexed

@@ -26,7 +26,6 @@ struct GateArgs {
     int n_params;
     const rn_half* dfrags;                       // [4][512] W0^T (input gradient), or null
     float* dx;                                   // (B,6) dL/dinput, or null
-    float* dw_part;                              // [n_blocks][n_params] block partials, or null
 };
 
 namespace {
@@ -299,29 +298,10 @@ k_gate_bwd(GateArgs a) {
         rn_lds_order();
     }
     __syncthreads();
-    if (a.dw_part) {
-        // the block's partial dW, summed over the blocks in a fixed order by
-        // k_gate_dw_sum: a run-to-run reproducible gate gradient (the atomic
-        // form below is faster: 0.091 vs 0.107 ms at 8192 rays)
-        float* part = a.dw_part + (int64_t)blockIdx.x * a.n_params;
-        for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) part[i] = sDW[i];
-        return;
-    }
     for (int i = threadIdx.x; i < a.n_params; i += blockDim.x) {
         const float v = sDW[i];
         if (v != 0.f) atomicAdd(&a.dw[i], v);
     }
-}
-
-// dw[i] += sum over the blocks' partials of k_gate_bwd, block order (the
-// gate's weight gradient is then run-to-run reproducible)
-__global__ void __launch_bounds__(256)
-k_gate_dw_sum(const float* __restrict__ part, int n_blocks, int n_params, float* __restrict__ dw) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n_params) return;
-    float s = 0.f;
-    for (int b = 0; b < n_blocks; ++b) s += part[(int64_t)b * n_params + i];
-    dw[i] += s;
 }
 
 }  // namespace
@@ -344,8 +324,7 @@ int rn_gate_fwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
 
 int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_rays, int32_t n_models,
                 const void* frags, const float* dL_dgate, float* dw, int32_t n_params,
-                const void* dinput_frags, float* dL_dinput, int32_t n_blocks, float* dw_partial,
-                void* stream) {
+                const void* dinput_frags, float* dL_dinput, int32_t n_blocks, void* stream) {
     RN_CHECK_ARG(n_rays >= 0 && n_models >= 1 && n_models <= 16 && n_blocks >= 1, "bad sizes");
     RN_CHECK_ARG(n_params == 12672 + 64 * n_models, "n_params mismatch");
     if (n_rays == 0) return 0;
@@ -357,14 +336,8 @@ int rn_gate_bwd(const float* in0, const float* in1, int32_t stride, int64_t n_ra
     a.n_params = n_params;
     RN_CHECK_ARG(!dL_dinput || dinput_frags, "the input gradient needs dinput_frags");
     a.dfrags = (const rn_half*)dinput_frags; a.dx = dL_dinput;
-    a.dw_part = dw_partial;
     k_gate_bwd<<<n_blocks, GATE_WAVES * 64, 0, (hipStream_t)stream>>>(a);
     RN_CHECK_LAUNCH();
-    if (dw_partial) {
-        k_gate_dw_sum<<<(n_params + 255) / 256, 256, 0, (hipStream_t)stream>>>(dw_partial, n_blocks,
-                                                                              n_params, dw);
-        RN_CHECK_LAUNCH();
-    }
     return 0;
 }
 

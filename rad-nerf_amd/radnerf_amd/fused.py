@@ -282,12 +282,6 @@ class FusedMLRenderer:
         # spanned 1.3-3.7 ms for a 0.09 ms kernel).  C3 step: early 5.037,
         # field 5.045, main 5.117 ms (tools/step_variants.py, r02)
         self.gate_bwd_at = "early"
-        # gate weight gradient: per-block partials summed in block order by a
-        # second launch (True: run-to-run reproducible), or every block's fp32
-        # atomics into gate_grad (default: 0.091 vs 0.107 ms at C3, and the
-        # kernel runs on the side stream beside composite_bw / field_bwd;
-        # profiles/r05/gate/)
-        self.gate_dw_partials = False
         # input gradients (dL/drays_o, dL/drays_d) in backward(): set by
         # _MLRenderFn when the rays require grad (--optimize_ext)
         self.input_grad = False
@@ -663,18 +657,11 @@ class FusedMLRenderer:
             frags = g.packed_frags()
             if stream is side:
                 side.wait_stream(main)
-            nb = max(1, min(128, (B + 127) // 128))
-            part = None                 # (gate_dw_partials: per-block partials)
-            if self.gate_dw_partials:
-                if getattr(w, "gate_part", None) is None or w.gate_part.numel() < nb * gate_grad.numel():
-                    w.gate_part = torch.empty(nb * gate_grad.numel(), device=dev)
-                w.gate_part.record_stream(stream)
-                part = w.gate_part.data_ptr()
             self._ev("gate_bwd", L.gate_bwd, rays_o.data_ptr(), gate_in2.data_ptr(), 3, B, G,
                      frags.data_ptr(), dgate.data_ptr(), gate_grad.data_ptr(),
                      gate_grad.numel(), None if gate_dfr is None else gate_dfr.data_ptr(),
-                     None if gate_dx is None else gate_dx.data_ptr(), nb, part,
-                     stream.cuda_stream, stream=stream)
+                     None if gate_dx is None else gate_dx.data_ptr(),
+                     max(1, min(128, (B + 127) // 128)), stream.cuda_stream, stream=stream)
 
         # gate backward: it only needs dL/dgate (combine_bw)
         gate_at = self.gate_bwd_at if self.gate_grad_here else None

@@ -503,7 +503,7 @@ class _GateFn(torch.autograd.Function):
             lib().gate_bwd(x.data_ptr(), x.data_ptr() + 12, 6, B, g.out_dim, frags.data_ptr(),
                            dgate.float().contiguous().data_ptr(), dw.data_ptr(), dw.numel(),
                            None if dfr is None else dfr.data_ptr(),
-                           None if dx is None else dx.data_ptr(), nb, None, _stream(x.device))
+                           None if dx is None else dx.data_ptr(), nb, _stream(x.device))
         return dx, dw, None
 
 

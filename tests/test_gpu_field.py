@@ -128,38 +128,6 @@ def test_gate_forward_backward(cuda, K):
     assert e <= 1.5e-3        # measured <= 5.2e-4
 
 
-@pytest.mark.parametrize("K", [2, 8])
-def test_gate_dw_partials_reproducible(cuda, K):
-    """rn_gate_bwd with dw_partial (per-block partials summed in block order)
-    equals the atomic form within fp32 summation order and is bitwise the
-    same from run to run."""
-    from radnerf_amd._lib import lib
-    g = Ray_Gate(K, seed=2)
-    with torch.no_grad():
-        g.params.copy_(torch.from_numpy(S.mlp_params(1, LY.gate_params(K), seed=6, scale=0.3)[0]))
-    g = g.to(cuda)
-    B = 8192
-    o, d = S.rays(B)
-    x = torch.from_numpy(np.concatenate([o, d], 1)).to(cuda).contiguous()
-    dg = torch.from_numpy(np.random.default_rng(3).normal(0, 1, (B, K)).astype(np.float32)).to(cuda)
-    frags = g.packed_frags()
-    nb = (B + 127) // 128
-    part = torch.empty(nb * g.params.numel(), device=cuda)
-    st = torch.cuda.current_stream().cuda_stream
-
-    def run(use_part):
-        dw = torch.zeros_like(g.params)
-        lib().gate_bwd(x.data_ptr(), x.data_ptr() + 12, 6, B, K, frags.data_ptr(), dg.data_ptr(),
-                       dw.data_ptr(), dw.numel(), None, None, nb,
-                       part.data_ptr() if use_part else None, st)
-        torch.cuda.synchronize()
-        return dw
-    a1, a2, atom = run(True), run(True), run(False)
-    assert torch.equal(a1, a2)
-    rel = float((a1 - atom).norm() / atom.norm())
-    assert rel <= 1e-6, rel
-
-
 def _seeds(n, seed):
     rng = np.random.default_rng(seed)
     return rng.normal(0, 1, n).astype(np.float32), rng.normal(0, 1, (n, 3)).astype(np.float32)

@@ -57,7 +57,7 @@ def test_arg_validation_without_gpu():
     with pytest.raises(RuntimeError, match="null pointer"):
         L.packbits(None, 8, 0.5, None, None)
     with pytest.raises(RuntimeError, match="n_params mismatch"):
-        L.gate_bwd(None, None, 3, 10, 2, None, None, None, 5, None, None, 1, None, None)
+        L.gate_bwd(None, None, 3, 10, 2, None, None, None, 5, None, None, 1, None)
     # level-partitioned forward: level groups come in eights, at most 8 sub-NeRFs
     lv = [None] * 6 + [8, 2] + [None] * 14 + [16, None]
     with pytest.raises(RuntimeError, match="rn_field_fwd_levels.*multiple of 8"):
