@@ -1685,7 +1685,14 @@ __global__ void __launch_bounds__(1024)
 k_field_mlp_planes(FieldArgs a, int K) {
     extern __shared__ __attribute__((aligned(16))) rn_half sWm[];   // [<= FM_LDS_K][24 frags]
     __shared__ LvTab sT;
+    // the K segments (first sample, count), read once: per tile they were a
+    // global round trip ahead of the tile's dependent loads
+    __shared__ int32_t sSeg[2][FM_KMAX];
     lv_stage(sT, a.gm);
+    if (threadIdx.x < K) {
+        sSeg[0][threadIdx.x] = a.seg_base[threadIdx.x];
+        sSeg[1][threadIdx.x] = a.seg_count[threadIdx.x];
+    }
     int first[FM_KMAX + 1];
     first[0] = 0;
     for (int k = 0; k < K; ++k)
@@ -1714,10 +1721,10 @@ k_field_mlp_planes(FieldArgs a, int K) {
             int k = kb;
             while (k < ke && u >= first[k + 1]) ++k;
             const int t = u - first[k];
-            const int n_k = a.seg_count[k];
+            const int n_k = sSeg[1][k];
             const int i = t * 32 + c;
             const bool valid = i < n_k;
-            const int64_t s = a.seg_base[k] + (valid ? i : 0);
+            const int64_t s = sSeg[0][k] + (valid ? i : 0);
             FwdState st;
             float ux, uy, uz;
             rn_lds_order();
