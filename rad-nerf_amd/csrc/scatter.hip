@@ -29,6 +29,12 @@ __device__ unsigned long long g_gb_cyc[8];
 
 namespace {
 
+// record loads of the sum pass: plain loads (0.729 -> 0.717 ms at C5 against
+// non-temporal ones); the bin pass keeps non-temporal loads of its pages (read
+// once: 1.107 vs 1.21 ms with plain loads; profiles/r05/ab/ab_ntld_*)
+__device__ __forceinline__ uint64_t gb_ld(const uint64_t* p) { return *p; }
+
+
 #define GB_SUM_THREADS 1024
 
 // THREADS per page; PF: the next page's records are loaded (all 8192, the
@@ -226,14 +232,14 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
             r0[j] = 0ull; r1[j] = 0ull;
             if (BIS == 0) {                                 // the run's lanes only
                 if ((uint32_t)lane < cnt[j])
-                    r0[j] = __builtin_nontemporal_load(pgp[j] + st[j] + lane);
+                    r0[j] = gb_ld(pgp[j] + st[j] + lane);
                 if ((uint32_t)lane + 64u < cnt[j])
-                    r1[j] = __builtin_nontemporal_load(pgp[j] + st[j] + 64u + lane);
+                    r1[j] = gb_ld(pgp[j] + st[j] + 64u + lane);
             } else {                                        // full-lane loads (timing)
                 if (BIS != 4 || cnt[j] != 0u)
-                    r0[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
+                    r0[j] = gb_ld(pgp[j] + min(st[j] + lane, GB_PAGE - 1u));
                 if (cnt[j] > 64u)
-                    r1[j] = __builtin_nontemporal_load(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
+                    r1[j] = gb_ld(pgp[j] + min(st[j] + 64u + lane, GB_PAGE - 1u));
             }
         }
 #pragma unroll
@@ -248,7 +254,7 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
                 for (int u = 0; u < 8; ++u) {
                     rr[u] = 0ull;
                     if (BIS == 0 ? o + 64u * u + lane < cnt[j] : o + 64u * u < cnt[j])
-                        rr[u] = __builtin_nontemporal_load(
+                        rr[u] = gb_ld(
                             pgp[j] + min(st[j] + o + 64u * u + lane, GB_PAGE - 1u));
                 }
 #pragma unroll
