@@ -321,6 +321,7 @@ struct Walk2 {
     // binned mode (GM 4): each level's open page in the pool and its fill,
     // and the levels' first entries (wave-uniform)
     uint32_t pgA, pgB, nA, nB, loffA, loffB;
+    bool started;          // the chunk's first step has been walked (wave-uniform)
 };
 
 __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
@@ -332,6 +333,7 @@ __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
     W.offA = W.offB = 0;
     W.cA = W.cB = 0u;
+    W.started = false;
 }
 
 // Exact integer accumulation of the grid gradient (IG mode).  Each record
@@ -666,7 +668,11 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
         const bool act = decltype(check)::value ? j < ne : true;
         const vf4 uc = un;
         const vf2 gc = gn;
-        const int nx = s_base + (j + 1 < ne ? j + 1 : 0);
+        // the next row, read unconditionally: row ne of a block is the next
+        // block's first row or the tail of sW / the rings (always inside the
+        // kernel's LDS), read but never used (a clamp to row 0 cost three
+        // VALU per step)
+        const int nx = s_base + j + 1;
         un = *(lds_cf4*)(sU + nx * 4);
         gn = *(lds_cf2*)(gcol + __umul24((uint32_t)nx, SG_STRIDE));   // u32 offset, not a u64 mad
         const LevelPos p = level_pos(lc.sc, uc.x, uc.y, uc.z);
@@ -675,18 +681,20 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
         const uint32_t X0 = p.gx + c0, X1 = p.gx + (c0 ^ 1u), Y = p.gy + cy, Z = p.gz + cz;
         const float fxm = 1.0f - p.fx;
         const float wy = cy ? p.fy : 1.0f - p.fy, wz = cz ? p.fz : 1.0f - p.fz;
-        // weight = wx * wy * wz in tcnn's dimension order
-        const float w0 = ((c0 ? p.fx : fxm) * wy) * wz;
-        const float w1 = ((c0 ? fxm : p.fx) * wy) * wz;
+        // weight = wx * wy * wz in tcnn's dimension order, both corners in
+        // packed fp32 (v_pk_mul_f32: the same roundings, half the issues)
+        const vf2 wx = {c0 ? p.fx : fxm, c0 ? fxm : p.fx};
+        const vf2 w01 = (wx * wy) * wz;
         const bool row = Y == W.ey && Z == W.ez;
         const bool same0 = row && X0 == W.ex0, same1 = row && X1 == W.ex1;
-        walk2_push(W, act && !same0 && W.ex0 != W2_NONE, act && !same1 && W.ex1 != W2_NONE,
-                   lc.off);
+        // W.ex0 / ex1 are W2_NONE (nothing to emit) exactly until the chunk's
+        // first walked step (W.started, wave-uniform: a lane active at a step
+        // was active at every earlier step of the chunk)
+        walk2_push(W, act && !same0 && W.started, act && !same1 && W.started, lc.off);
         if (act) {
-            W.a00 = (same0 ? W.a00 : 0.f) + w0 * gc.x;
-            W.a01 = (same0 ? W.a01 : 0.f) + w0 * gc.y;
-            W.a10 = (same1 ? W.a10 : 0.f) + w1 * gc.x;
-            W.a11 = (same1 ? W.a11 : 0.f) + w1 * gc.y;
+            const vf2 p0 = vf2{same0 ? W.a00 : 0.f, same0 ? W.a01 : 0.f} + w01.x * gc;
+            const vf2 p1 = vf2{same1 ? W.a10 : 0.f, same1 ? W.a11 : 0.f} + w01.y * gc;
+            W.a00 = p0.x; W.a01 = p0.y; W.a10 = p1.x; W.a11 = p1.y;
             // tcnn grid_index with the row part shared by the two entries;
             // branch-free dense / hashed select (the two levels of a wave differ)
             const uint32_t db = __umul24(Y, lc.res) + __umul24(Z, lc.res2);
@@ -699,8 +707,15 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
             W.ex0 = X0; W.ex1 = X1; W.ey = Y; W.ez = Z;
         }
         walk2_drain<GM>(W, 32u, grad_rs, G, dbg);
+        W.started = true;
     };
     int j = 0;                                            // wave-uniform trip counts
+    // two steps per trip: the loop-carried rows and entries stay in their
+    // registers (one step per trip copied them back every step)
+    for (; j + 1 < nmin; j += 2) {
+        step(j, std::integral_constant<bool, false>{});
+        step(j + 1, std::integral_constant<bool, false>{});
+    }
     for (; j < nmin; ++j) step(j, std::integral_constant<bool, false>{});
     for (; j < n0; ++j) step(j, std::integral_constant<bool, true>{});
 }
