@@ -762,11 +762,14 @@ __device__ __forceinline__ void grid_scatter_block(const FieldArgs& a, const LvT
 // operands (lgkmcnt counts in issue order).  Written as one load per step
 // followed by its MFMA, the compiler waited lgkmcnt(0) before every MFMA and
 // the 16-step tile took 16 LDS round trips (round 5, field.hip ISA).
+// (NS < 16, steps [j0, j0 + NS) only: the balanced-dW timing study, flag 1024)
 #define DW_DEPTH 3
-__device__ __forceinline__ f32x16 dw_block_tile(const rn_half* sImg, int ya, int xa, f32x16 acc) {
-    constexpr int NS = 2 * BWD_WAVES;                 // 16 steps of 16 samples
+template <int NS = 2 * BWD_WAVES>                     // 16 steps of 16 samples
+__device__ __forceinline__ f32x16 dw_block_tile(const rn_half* sImg, int ya, int xa, f32x16 acc,
+                                                int j0 = 0) {
     half8 ys[DW_DEPTH], xs[DW_DEPTH];
     auto load = [&](int j, half8& y, half8& x) {
+        j += j0;
         const rn_half* iy = sImg + (j >> 1) * 2 * RN_IMG_HALFS;
         y = rn_img_read(iy, ya, j & 1);
         x = rn_img_read(iy + RN_IMG_HALFS, xa, j & 1);
@@ -839,6 +842,12 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
                                              const float* pre = nullptr) {
     const int lane = rn_lane(), h = lane >> 5;
     const half8 z8 = rn_zero8();
+    // timing study only (ablation build, flag 1024; WRONG dW): every layer's
+    // dW tiles contracted by all 8 waves, each over its share of the samples
+    // (2-tile layers: 4 of the 16 steps, waves w and w + 4 on one SIMD take
+    // the same tile), all into the wave's own accumulators -- the MFMA / LDS
+    // schedule of a balanced dW ownership without its registers
+    const bool bal = rn_dbg(a.dbg) & 1024;
     // ---- seeds (lanes h == 0 own the output rows); `pre`: dL/dsigma and
     // dL/drgb already loaded by the caller (ahead of the forward recompute)
     float o0 = 0.f, o1 = 0.f, o2 = 0.f, gsig = 0.f;
@@ -894,7 +903,8 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.r2[q]);
     }
     if (sync) __syncthreads();                                                    // B1
-    if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
+    if (do_dw && bal) accA = dw_block_tile<4>(sImg, 0, 32 * (wid & 1), accA, 4 * (wid >> 1));
+    else if (do_dw && wid < 2) accA = dw_block_tile(sImg, 0, 32 * wid, accA);
     half8 dr2f[4];
     {
         f32x16 b0 = rn_zero16(), b1 = rn_zero16();
@@ -910,7 +920,9 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         for (int q = 0; q < 4; ++q) { rn_img_write(imgY, q, dr2f[q]); rn_img_write(imgX, q, st.r1[q]); }
     }
     if (sync) __syncthreads();                                                    // B3
-    if (do_dw && wid >= 2 && wid < 6)
+    if (do_dw && bal)
+        accA = dw_block_tile<8>(sImg, 32 * ((wid & 3) >> 1), 32 * (wid & 1), accA, 8 * (wid >> 2));
+    else if (do_dw && wid >= 2 && wid < 6)
         accA = dw_block_tile(sImg, 32 * ((wid - 2) >> 1), 32 * ((wid - 2) & 1), accA);
     half8 dr1f[4];
     {
@@ -931,7 +943,8 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         rn_img_write(imgX, 0, st.sh); rn_img_write(imgX, 1, st.gin);
     }
     if (sync) __syncthreads();                                                    // B5
-    if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
+    if (do_dw && bal) accA = dw_block_tile<4>(sImg, 32 * (wid & 1), 0, accA, 4 * (wid >> 1));
+    else if (do_dw && wid >= 6) accA = dw_block_tile(sImg, 32 * (wid - 6), 0, accA);
     half8 dg0, dg1;
     {
         f32x16 b = rn_zero16();
@@ -949,7 +962,8 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         for (int q = 0; q < 4; ++q) rn_img_write(imgX, q, st.h1[q]);
     }
     if (sync) __syncthreads();                                                    // B7
-    if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
+    if (do_dw && bal) accB = dw_block_tile<4>(sImg, 0, 32 * (wid & 1), accB, 4 * (wid >> 1));
+    else if (do_dw && wid < 2) accB = dw_block_tile(sImg, 0, 32 * wid, accB);
     half8 dh1f[4];
     {
         f32x16 b0 = rn_zero16(), b1 = rn_zero16();
@@ -966,7 +980,8 @@ __device__ __forceinline__ f32x16 bwd_window(const FieldArgs& a, const rn_half* 
         rn_img_write(imgX, 0, st.e0); rn_img_write(imgX, 1, st.e1);
     }
     if (sync) __syncthreads();                                                    // B9
-    if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
+    if (do_dw && bal) accB = dw_block_tile<4>(sImg, 32 * (wid & 1), 0, accB, 4 * (wid >> 1));
+    else if (do_dw && (wid == 2 || wid == 3)) accB = dw_block_tile(sImg, 32 * (wid - 2), 0, accB);
     f32x16 dE = rn_zero16();
 #pragma unroll
     for (int q = 0; q < 4; ++q) dE = rn_mfma(rn_frag(sW, 42 + q), dh1f[q], dE);
