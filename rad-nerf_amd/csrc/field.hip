@@ -424,7 +424,7 @@ __device__ __forceinline__ uint32_t w2_wrap(uint32_t v) { return v >= W2_RING ? 
 // wid) selects its scale, page and statistics registers at compile time (as a
 // runtime select the compiler emitted both paths with ~12 register copies of
 // the 64-bit sums per issue)
-template <int GM, bool ODD, bool FULL = false>
+template <int GM, bool ODD, bool FULL = false, bool DEFER = false>
 __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
                                             __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                             int dbg) {
@@ -544,9 +544,11 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
     if (GM == 4 && fx_lvl) {
         if (odd) W.nB += cnt; else W.nA += cnt;
     }
-    const bool me = (lane >> 2) == s;                     // selects, not a branch
-    W.head = me ? w2_wrap(W.head + cnt) : W.head;
-    W.pend = me ? W.pend - cnt : W.pend;
+    if (!DEFER) {           // (DEFER: the threshold drain advances every issued ring at once)
+        const bool me = (lane >> 2) == s;                 // selects, not a branch
+        W.head = me ? w2_wrap(W.head + cnt) : W.head;
+        W.pend = me ? W.pend - cnt : W.pend;
+    }
 }
 
 // integer mode: settle the two outstanding issues (end of a chunk)
@@ -576,7 +578,7 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
                 const int s = __builtin_ctzll(mm) >> 2;
                 const uint32_t p = __builtin_amdgcn_readlane(pend, 4 * s);
                 if (min_cnt >= 32u)     // threshold drain (constant after inlining): p >= 32
-                    walk2_issue<GM, O, true>(W, s, 32u, grad_rs, G, dbg);
+                    walk2_issue<GM, O, true, true>(W, s, 32u, grad_rs, G, dbg);
                 else
                     walk2_issue<GM, O>(W, s, p < 32u ? p : 32u, grad_rs, G, dbg);
                 mm &= mm - 1;
@@ -584,7 +586,16 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
         };
         run(m & 0x0101010101010101ull, std::integral_constant<bool, false>{});
         run(m & 0x1010101010101010ull, std::integral_constant<bool, true>{});
-        if (min_cnt > 0u) break;      // threshold drain: what remains is < 32
+        if (min_cnt > 0u) {
+            // threshold drain: every ring with >= 32 pending issued exactly 32
+            // (head / pend of a stream are the same on its 4 lanes), advanced
+            // here once instead of by selects after every issue; what remains
+            // is < 32
+            const bool did = pend >= 32u;
+            W.head = did ? w2_wrap(W.head + 32u) : W.head;
+            W.pend = did ? pend - 32u : pend;
+            break;
+        }
     }
 }
 
