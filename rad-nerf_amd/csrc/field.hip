@@ -467,7 +467,10 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
     if (FULL || (uint32_t)lane < 2u * cnt) {
         const uint32_t rec = w2_wrap(h + (lane >> 1));
         const uint32_t* base = W.ring + s * 3 * W2_RING;
-        const uint32_t off = base[rec] + 4u * (lane & 1);
+        const uint32_t w0 = base[rec];
+        // byte offset of the lane's feature (GM 4: only the fp32 fallback
+        // and the timing branches use it; the page record takes w0)
+        const uint32_t off = (GM == 4 ? 8u * ((odd ? W.loffB : W.loffA) + w0) : w0) + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
         if (rn_dbg(dbg) & 1) {
             asm volatile("" :: "v"(off), "v"(v));
@@ -484,17 +487,16 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             // e5m17 (rn_bin.h); a record at or past 2^46 units saturates and
             // vmax flags the step for the fp32 redo
-            const int q = (int)gb_encode(__uint_as_float(v) * sc_s);
-            const int qp = __builtin_amdgcn_mov_dpp(q, 0xb1, 0xf, 0xf, true);   // partner lane ^ 1
-            // both words on every lane, then a select: with the index read
-            // only on the even lanes the compiler branched on lane & 1 (an
-            // exec-mask if / else per issue)
-            const uint32_t idx = (off >> 3) - (odd ? W.loffB : W.loffA);
+            const uint32_t q = gb_encode_walk(__uint_as_float(v) * sc_s);
+            const uint32_t qp = (uint32_t)__builtin_amdgcn_mov_dpp((int)q, 0xb1, 0xf, 0xf, true);   // partner lane ^ 1
+            // lane 2r: entry | q0 << 20 (q0 = its own q); lane 2r + 1:
+            // q0 >> 12 (the partner's) | q1 << 10 (its own): one shift-or
+            // with a per-lane shift and a select, no branch on lane & 1
+            // (w0 < the level's size <= 2^GB_IDX_BITS: the walk's hash /
+            // dense index is reduced mod the size)
             const bool hi_lane = lane & 1;
-            const uint32_t q0 = (uint32_t)(hi_lane ? qp : q), q1 = (uint32_t)(hi_lane ? q : qp);
-            const uint32_t w_hi = ((q0 >> 12) & 0x3ffu) | (q1 << 10);
-            const uint32_t w_lo = (idx & ((1u << GB_IDX_BITS) - 1u)) | (q0 << 20);
-            const uint32_t word = hi_lane ? w_hi : w_lo;
+            const uint32_t lowbits = hi_lane ? (qp >> 12) & 0x3ffu : w0;
+            const uint32_t word = (q << (hi_lane ? 10u : 20u)) | lowbits;
             const uint32_t pg = odd ? W.pgB : W.pgA, n = odd ? W.nB : W.nA;
             uint32_t* dst = reinterpret_cast<uint32_t*>(G.pages + (size_t)pg * GB_PAGE + n) + lane;
             if (pg < G.pool_pages) {
@@ -603,6 +605,10 @@ __device__ __forceinline__ void walk2_drain(Walk2& W, uint32_t min_cnt,
 // lane-major (a lane's even-X and odd-X records adjacent: they share a 64-B
 // segment, so an instruction boundary splits them less often; replay of the
 // bench samples, tools/atomic_sim2.py: 15.18 -> 14.65 requests/sample)
+// Ring word 0 of a record: the byte offset 8 (level offset + entry) of its
+// first feature in the grid (GM 4: the entry index within the level, what a
+// page record holds)
+template <int GM>
 __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t lvl_off) {
     // a stream's 4 lanes are one DPP quad: the lane's first record index is
     // the exclusive quad prefix of the per-lane record counts (two quad_perm
@@ -623,10 +629,10 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t 
     // ring; it is overwritten before it is ever read)
     const uint32_t r0 = w2_wrap(W.tail + (e0 ? below : pushed));
     const uint32_t r1 = w2_wrap(W.tail + (e1 ? below + (e0 ? 1u : 0u) : pushed));
-    base[r0] = 8u * (lvl_off + W.cur0);
+    base[r0] = GM == 4 ? W.cur0 : 8u * (lvl_off + W.cur0);
     base[W2_RING + r0] = __float_as_uint(W.a00);
     base[2 * W2_RING + r0] = __float_as_uint(W.a01);
-    base[r1] = 8u * (lvl_off + W.cur1);
+    base[r1] = GM == 4 ? W.cur1 : 8u * (lvl_off + W.cur1);
     base[W2_RING + r1] = __float_as_uint(W.a10);
     base[2 * W2_RING + r1] = __float_as_uint(W.a11);
     W.tail = w2_wrap(W.tail + pushed);
@@ -701,7 +707,7 @@ __device__ __forceinline__ void walk2_window(const FieldArgs& a, const LvTab& sT
         // W.ex0 / ex1 are W2_NONE (nothing to emit) exactly until the chunk's
         // first walked step (W.started, wave-uniform: a lane active at a step
         // was active at every earlier step of the chunk)
-        walk2_push(W, act && !same0 && W.started, act && !same1 && W.started, lc.off);
+        walk2_push<GM>(W, act && !same0 && W.started, act && !same1 && W.started, lc.off);
         if (act) {
             const vf2 p0 = vf2{same0 ? W.a00 : 0.f, same0 ? W.a01 : 0.f} + w01.x * gc;
             const vf2 p1 = vf2{same1 ? W.a10 : 0.f, same1 ? W.a11 : 0.f} + w01.y * gc;
@@ -737,7 +743,7 @@ __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
                                           __amdgpu_buffer_rsrc_t grad_rs, const IntGrad& G,
                                           Walk2& W, int dbg) {
     const LvConst lc = walk2_level(a, sT);
-    walk2_push(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, lc.off);
+    walk2_push<GM>(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, lc.off);
     walk2_drain<GM>(W, 0u, grad_rs, G, dbg);
     if (GM == 1) walk2_settle(W, G);
     W.swA -= (uint64_t)W.cA << 32;          // the negative records' 2^32 w terms

@@ -64,6 +64,17 @@ __host__ __device__ __forceinline__ uint32_t gb_encode(float x) {
     const float y = fminf(fmaxf(rintf(ldexpf(x, -e)), -32768.f), 32768.f);
     return ((uint32_t)(int)y & ((1u << GB_M_BITS) - 1u)) | ((uint32_t)e << GB_M_BITS);
 }
+// The walk's form (field.hip GM 4): the same word for every |x| < 2^46 units
+// (there |m| <= 2^15 needs no clamp); a record at or past 2^46, or NaN, sets
+// the redo flag through the level's vmax (k_fx_check), and the step's pages
+// are discarded, so its word need not saturate
+__device__ __forceinline__ uint32_t gb_encode_walk(float x) {
+    const uint32_t E = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;
+    int e = (int)E - (127 + 14);
+    e = e < 0 ? 0 : (e > GB_E_MAX ? GB_E_MAX : e);
+    const int m = (int)rintf(ldexpf(x, -e));
+    return ((uint32_t)m & ((1u << GB_M_BITS) - 1u)) | ((uint32_t)e << GB_M_BITS);
+}
 __host__ __device__ __forceinline__ int64_t gb_decode(uint32_t f) {
     const int64_t m = (int64_t)((int32_t)(f << (32 - GB_M_BITS)) >> (32 - GB_M_BITS));
     return m * ((int64_t)1 << ((f >> GB_M_BITS) & (uint32_t)GB_E_MAX));
