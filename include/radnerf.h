@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 6   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 7   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -251,9 +251,9 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * |record|), u32 emax[16] (rn_grid_fx_fold: the level's largest |int32 entry|),
  * i64 qsum[16] (the exact sum of each level's integer records), i64 esum[16]
  * (rn_grid_fx_fold: the exact sum of the level's int32 entries), u64 wq[16]
- * and we[16] (the same sums with each element i weighted by
- * ((i mod 2^24) * 0x9E3779) mod 2^32, mod 2^64; fixed point needs a grid of at
- * most 2^24 gradient elements, so the weight is injective).
+ * and we[16] (the same sums with each element i weighted by its byte offset
+ * 4 i, mod 2^64; fixed point needs a grid of at most 2^28 gradient elements,
+ * so the weight is injective below 2^30).
  * Each record goes in as rint(v * 2^e_l) with non-returning u32 atomics (the
  * memory side serves them ~27 % faster than f32 adds), so those levels'
  * gradients are order-independent and bitwise reproducible.

@@ -313,11 +313,6 @@ struct Walk2 {
     // (fx_weight): two entries that wrap in opposite directions cancel in
     // the plain sum but not in this one
     uint64_t swA, swB;
-    // ... accumulated as unsigned products q_u32 * w (one 32x32 -> 64 mad per
-    // record); the sum of w over the negative records, times 2^32, is taken
-    // off at the end of the walk (walk2_end): (int64) q * w = q_u32 * w -
-    // [q < 0] w 2^32 mod 2^64
-    uint32_t cA, cB;
     // binned mode (GM 4): each level's open page in the pool and its fill,
     // and the levels' first entries (wave-uniform)
     uint32_t pgA, pgB, nA, nB, loffA, loffB;
@@ -332,7 +327,6 @@ __device__ __forceinline__ void walk2_begin(Walk2& W, uint32_t* ring) {
     // after its last issue, so they are not reset here)
     W.oldA = W.loA = W.hiA = W.oldB = W.loB = W.hiB = 0;
     W.offA = W.offB = 0;
-    W.cA = W.cB = 0u;
     W.started = false;
 }
 
@@ -394,17 +388,16 @@ struct FxStats {           // rn_grid_fx_fold / rn_field_bwd_merged fx_stats blo
 static_assert(sizeof(FxStats) == RN_FX_STATS_BYTES, "FxStats layout (include/radnerf.h)");
 
 // weight of grid-gradient element i (an int32 of the fixed-point table) in the
-// position-weighted checksums: a bijection of i mod 2^32 (odd multiplier), so
-// wraps of +-2^32 on two different elements a, b cancel only if w_a == w_b
-// (mod 2^32), i.e. never
-// A 24-bit multiply (full rate; a 32-bit one is quarter rate on the walk's
-// issue path): i < 2^24 (rn_field_bwd_merged refuses fixed point for larger
-// tables) and the odd multiplier keep w injective, since (a - b) * M = 0
-// mod 2^32 only for a = b
-#define FX_WEIGHT_M 0x9E3779u
-__host__ __device__ __forceinline__ uint32_t fx_weight(uint32_t i) {
-    return (i & 0xffffffu) * FX_WEIGHT_M;          // = __umul24(i, M): low 32 bits
-}
+// position-weighted checksums: its byte offset 4 i, which the walk's issue
+// already holds (no multiply on the issue path).  Wraps of +-2^32 on two
+// different elements a, b move the weighted sum by 2^34 (a - b) mod 2^64,
+// which is 0 only for a = b mod 2^30: never on a table of at most 2^28
+// elements (rn_field_bwd_merged refuses fixed point for larger ones).  (Any
+// injective weight is linear in the same way for three or more wraps: round
+// 5's odd multiplier, (i mod 2^24) * 0x9E3779, cancelled exactly when
+// sum(+-i) = 0 mod 2^32, like this one.)  The weights are < 2^30, so the
+// walk adds q * w with one signed 32 x 32 -> 64 mad.
+__host__ __device__ __forceinline__ uint32_t fx_weight(uint32_t i) { return 4u * i; }
 
 struct FxGrad {
     int32_t* acc;              // int32 [entries][2]
@@ -519,11 +512,10 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             else
                 __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(__uint_as_float(v), grad_rs,
                                                             (int)off, 0, 0);
-            const uint32_t w = fx_weight(off >> 2);
-            const uint32_t neg = w & (uint32_t)(q >> 31);
-            const uint64_t qw = (uint64_t)(uint32_t)q * (uint64_t)w;
-            if (odd) { W.sqB += (int64_t)q; W.swB += qw; W.cB += neg; }
-            else { W.sqA += (int64_t)q; W.swA += qw; W.cA += neg; }
+            // off = 4 x element = fx_weight(element) < 2^30: one v_mad_i64_i32
+            const int64_t qw = (int64_t)q * (int64_t)(int32_t)off;
+            if (odd) { W.sqB += (int64_t)q; W.swB += (uint64_t)qw; }
+            else { W.sqA += (int64_t)q; W.swA += (uint64_t)qw; }
         } else if (GM == 1) {
             // exact: |v * 2^e| < 2^62 for any finite gradient the scale admits
             const float x = rintf(__uint_as_float(v) * G.scale);
@@ -746,8 +738,6 @@ __device__ __forceinline__ void walk2_end(const FieldArgs& a, const LvTab& sT,
     walk2_push<GM>(W, W.ex0 != W2_NONE, W.ex1 != W2_NONE, lc.off);
     walk2_drain<GM>(W, 0u, grad_rs, G, dbg);
     if (GM == 1) walk2_settle(W, G);
-    W.swA -= (uint64_t)W.cA << 32;          // the negative records' 2^32 w terms
-    W.swB -= (uint64_t)W.cB << 32;
     walk2_begin(W, W.ring);
 }
 
@@ -2520,10 +2510,11 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                  perm && chunk_desc && queue && grid_f16 && level_offset && level_hsize && level_res &&
                  level_scale && xyz_min && extent && frags && dL_dsigma && dL_drgb && grid_grad &&
                  dw && scratch && park, "null pointer");
-    // fixed point: the wrap checksum's element weights are 24-bit (fx_weight)
+    // fixed point: the wrap checksum's element weights 4 i (fx_weight) stay
+    // injective and below 2^30 up to 2^28 elements
     RN_CHECK_ARG(fx_mode != 2 ||
-                 2ull * ((uint64_t)level_offset[RN_L - 1] + level_hsize[RN_L - 1]) <= (1ull << 24),
-                 "fixed-point mode: the grid has more than 2^24 gradient elements");
+                 2ull * ((uint64_t)level_offset[RN_L - 1] + level_hsize[RN_L - 1]) <= (1ull << 28),
+                 "fixed-point mode: the grid has more than 2^28 gradient elements");
     FieldArgs a{};
     fill_args(a, xyz_min, extent, level_offset, level_hsize, level_res, level_scale);
     a.dbg = rn_dbg(g_field_dbg);

@@ -74,7 +74,8 @@ extern "C" {
 // wrap checksums wq / we weight element i by ((i mod 2^24) * 0x9E3779) mod
 // 2^32 (a 24-bit multiply), fx_mode 2 refuses grids over 2^24 elements.  6
 // (round 5) rn_bwd_plan takes balance_blocks (big chunks a multiple of the
-// persistent blocks in number).
+// persistent blocks in number).  7 (round 5) wq / we weight element i by its
+// byte offset 4 i; fx_mode 2 takes grids up to 2^28 elements.
 int rn_version(void) { return RN_ABI_VERSION; }
 
 const char* rn_last_error(void) { return g_err; }

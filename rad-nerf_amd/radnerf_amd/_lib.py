@@ -94,7 +94,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 _lib = None
 
 

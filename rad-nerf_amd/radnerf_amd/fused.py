@@ -257,11 +257,11 @@ class FusedMLRenderer:
         # of memory-side atomics, which were 45 % of C5's field_bwd
         # (DESIGN §4 "Binned scatter")
         self.grid_bin = self.grid_fx and float(model.scale) > 0.5
-        # the int32 form's wrap checksums weight gradient elements by a 24-bit
-        # multiply (field.hip fx_weight): a larger table (none of the
-        # reference's configs: 16 levels x 2^19 entries x 2 features = 2^24)
-        # keeps fp32 atomics unless it is binned (no checksum there)
-        if not self.grid_bin and model.xyz_encoder.params.numel() > (1 << 24):
+        # the int32 form's wrap checksums weight gradient element i by 4 i
+        # (field.hip fx_weight), injective up to 2^28 elements: a larger table
+        # (none of the reference's configs: 16 levels x 2^19 entries x 2
+        # features = 2^24) keeps fp32 atomics unless it is binned (no checksum)
+        if not self.grid_bin and model.xyz_encoder.params.numel() > (1 << 28):
             self.grid_fx = False
         # initial pool: records per (ray, sub-NeRF) at scale 16 (C5's replay:
         # 63.5 records x 95 samples; tools/records_sim.py), x 1.15

@@ -221,7 +221,7 @@ def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
 
 
 def _fx_weight(i):
-    return ((int(i) & 0xFFFFFF) * 0x9E3779) & 0xFFFFFFFF   # fx_weight (field.hip)
+    return (4 * int(i)) & 0xFFFFFFFF                       # fx_weight (field.hip): byte offset
 
 
 @pytest.mark.parametrize("wrapped", [True, False])
@@ -229,7 +229,7 @@ def test_fx_opposite_wraps_set_redo(cuda, wrapped):
     """ADVICE r03 / VERDICT r03 item 5: two int32 entries of one level that wrap
     in opposite directions in one step (+2^32 and -2^32) leave the level's
     plain entry sum equal to its record sum; the position-weighted sums
-    (element i weighted by ((i mod 2^24) * 0x9E3779) mod 2^32, mod 2^64) still differ,
+    (element i weighted by its byte offset 4 i, mod 2^64) still differ,
     so rn_grid_fx_fold sets the redo flag.  Control: the same records without
     a wrap pass."""
     from radnerf_amd._lib import lib

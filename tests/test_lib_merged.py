@@ -150,27 +150,31 @@ def test_grid_record_e5m17_format():
 
 
 def test_fx_mode_refuses_grids_past_the_checksum_weights():
-    """fx_mode 2's wrap checksums weight element i by a 24-bit multiply
-    (field.hip fx_weight): a grid of more than 2^24 gradient elements is
-    refused before any HIP call; the reference's largest grid (16 levels x
-    2^19 entries x 2 features = 2^24) passes that check."""
+    """fx_mode 2's wrap checksums weight element i by its byte offset 4 i
+    (field.hip fx_weight), injective below 2^30: a grid of more than 2^28
+    gradient elements is refused before any HIP call."""
     import numpy as np
     L = _lib.lib()
     V = ctypes.c_void_p(8)
-    off = np.arange(16, dtype=np.uint32) * (1 << 19)
-    hs = np.full(16, 1 << 19, np.uint32)
+    off = np.arange(16, dtype=np.uint32) * (1 << 23)
+    hs = np.full(16, 1 << 23, np.uint32)
     big = hs.copy()
     big[-1] += 1
     args = lambda h: [*[V] * 10, 8, 2, 1024, V, off.ctypes.data, h.ctypes.data, *[V] * 11, 4096, V,
                       1024, 256, None, None, None, V, V, V, V, 2, None, None, None, 0, None]
-    with pytest.raises(RuntimeError, match="more than 2\\^24 gradient elements"):
+    with pytest.raises(RuntimeError, match="more than 2\\^28 gradient elements"):
         L.field_bwd_merged(*args(big))
 
 
-def test_fx_weight_is_injective_on_24_bits():
-    """the checksum weight ((i mod 2^24) * 0x9E3779) mod 2^32 takes 2^24
-    distinct values on i < 2^24 (opposite wraps on two elements never cancel)"""
+def test_fx_weight_separates_opposite_wraps():
+    """opposite +-2^32 wraps on elements a != b move the weighted sum by
+    2^32 (w_a - w_b) mod 2^64 with w = 4 i: non-zero for every pair of a
+    2^28-element table (the weight's difference is 4 (a - b), 0 < |a - b| <
+    2^28)"""
     import numpy as np
-    i = np.arange(1 << 24, dtype=np.uint64)
-    w = (i * 0x9E3779) & 0xFFFFFFFF
-    assert len(np.unique(w)) == 1 << 24
+    rng = np.random.default_rng(5)
+    a = rng.integers(0, 1 << 28, 100000, dtype=np.uint64)
+    b = rng.integers(0, 1 << 28, 100000, dtype=np.uint64)
+    keep = a != b
+    d = ((a[keep] * 4) - (b[keep] * 4)) << np.uint64(32)    # mod 2^64
+    assert np.all(d != 0)
