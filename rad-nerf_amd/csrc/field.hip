@@ -2012,22 +2012,77 @@ k_fx_fold(int64_t e0, int64_t e1, GridMeta gm, const float* __restrict__ scale,
 #define PLAN_WAVES 4
 #define PLAN_LDS 2048      // floats per wave
 
+// Stage one ray's K runs of t (and, with ids, each sample's position in the
+// concatenation) into the wave's LDS slice: position i of the concatenated
+// runs [bnd[k], bnd[k+1]) is sample off[k] + i - bnd[k].  Positions are dealt
+// over the lanes with PLAN_UNR loads in flight per lane (a loop per run, one
+// load then its store, waited for each load: 16 round trips per ray at K = 8,
+// and k_bwd_plan_multi took 0.139 ms at C5).  bnd / off are wave-uniform.
+#define PLAN_UNR 8
+
+// Ray r's run of each model (count, first sample) and its merged start ms.
+// r is wave-uniform (the wave id read back as a scalar), and every model's
+// words load unconditionally (index clamped to K - 1, zeroed after): scalar
+// loads issued together.  (With the wave id a vector value and each load
+// under k < K, the 2K counts / offsets became vector loads waited for one by
+// one: ~16 round trips per ray at K = 8.)
+__device__ __forceinline__ void plan_ray_runs(int K, int B, int r, const int32_t* __restrict__ counts,
+                                              const int32_t* __restrict__ offsets,
+                                              const int32_t* __restrict__ seg_base, int* cnt,
+                                              int* off, int& ms) {
+    int c[MB_KMAX], o[MB_KMAX], sb[MB_KMAX];
+#pragma unroll
+    for (int k = 0; k < MB_KMAX; ++k) {
+        const int kk = k < K ? k : K - 1;
+        c[k] = counts[kk * B + r]; o[k] = offsets[kk * B + r]; sb[k] = seg_base[kk];
+    }
+    ms = 0;
+#pragma unroll
+    for (int k = 0; k < MB_KMAX; ++k) {
+        cnt[k] = k < K ? c[k] : 0;
+        off[k] = k < K ? o[k] : 0;
+        ms += k < K ? o[k] - sb[k] : 0;
+    }
+}
+__device__ __forceinline__ void plan_stage(int K, int tot_r, const int* bnd, const int* off,
+                                           const float* __restrict__ ts, float* st, uint16_t* si) {
+    const int lane = rn_lane();
+    for (int i0 = 0; i0 < tot_r; i0 += RN_WAVE * PLAN_UNR) {
+        float v[PLAN_UNR];
+#pragma unroll
+        for (int u = 0; u < PLAN_UNR; ++u) {
+            const int i = i0 + u * RN_WAVE + lane;
+            int base = off[0];                    // off[k] - bnd[k] of i's run (bnd[0] = 0)
+#pragma unroll
+            for (int kq = 1; kq < MB_KMAX; ++kq)
+                base = (kq < K && i >= bnd[kq]) ? off[kq] - bnd[kq] : base;
+            v[u] = i < tot_r ? ts[base + i] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < PLAN_UNR; ++u) {
+            const int i = i0 + u * RN_WAVE + lane;
+            if (i < tot_r) {
+                st[i] = v[u];
+                if (si) si[i] = (uint16_t)i;
+            }
+        }
+    }
+}
+
 __global__ void __launch_bounds__(PLAN_WAVES * 64)
 k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
            const int32_t* __restrict__ seg_base, const int32_t* __restrict__ seg_count,
            const float* __restrict__ ts, int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
     __shared__ float sT[PLAN_WAVES][PLAN_LDS];
-    const int wid = threadIdx.x / RN_WAVE;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int r = blockIdx.x * PLAN_WAVES + wid;
     if (r >= B) return;                      // wave-uniform; no block barrier below
     const int lane = rn_lane();
     int ms = 0, tot_r = 0;
     int cnt[MB_KMAX], off[MB_KMAX], loc[MB_KMAX];
-    for (int k = 0; k < K; ++k) {
-        cnt[k] = counts[k * B + r]; off[k] = offsets[k * B + r];
-        ms += off[k] - seg_base[k];
-        loc[k] = tot_r; tot_r += cnt[k];
-    }
+    plan_ray_runs(K, B, r, counts, offsets, seg_base, cnt, off, ms);
+#pragma unroll
+    for (int k = 0; k < MB_KMAX; ++k) { loc[k] = tot_r; tot_r += cnt[k]; }
     if (lane == 0) {
         mstart[r] = ms;
         if (r == 0) {
@@ -2039,8 +2094,7 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
     const bool staged = tot_r <= PLAN_LDS;
     float* st = sT[wid];
     if (staged) {
-        for (int k = 0; k < K; ++k)
-            for (int i = lane; i < cnt[k]; i += RN_WAVE) st[loc[k] + i] = ts[off[k] + i];
+        plan_stage(K, tot_r, loc, off, ts, st, nullptr);
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     }
@@ -2144,19 +2198,16 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
     __shared__ float sT[PLANM_WAVES][2][PLANM_LDS];
     __shared__ uint16_t sI[PLANM_WAVES][2][PLANM_LDS];
     static_assert(PLANM_LDS <= 65536, "u16 sample ids");
-    const int wid = threadIdx.x / RN_WAVE;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int r = blockIdx.x * PLANM_WAVES + wid;
     if (r >= B) return;                      // wave-uniform; no block barrier below
     const int lane = rn_lane();
     int ms = 0, tot_r = 0;
-    int bnd[MB_KMAX + 1], off[MB_KMAX];
-    for (int k = 0; k < K; ++k) {
-        const int c = counts[k * B + r];
-        off[k] = offsets[k * B + r];
-        ms += off[k] - seg_base[k];
-        bnd[k] = tot_r; tot_r += c;
-    }
-    bnd[K] = tot_r;
+    int bnd[MB_KMAX + 1], off[MB_KMAX], cnt[MB_KMAX];
+    plan_ray_runs(K, B, r, counts, offsets, seg_base, cnt, off, ms);
+#pragma unroll
+    for (int k = 0; k < MB_KMAX; ++k) { bnd[k] = tot_r; tot_r += cnt[k]; }
+    bnd[MB_KMAX] = tot_r;
     if (lane == 0) {
         mstart[r] = ms;
         if (r == 0) {
@@ -2191,11 +2242,7 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
     int kb[MB_KMAX];                          // the models' runs (bnd is merged below)
 #pragma unroll
     for (int k = 0; k < MB_KMAX; ++k) kb[k] = k < K ? bnd[k] : 0;
-    for (int k = 0; k < K; ++k)
-        for (int i = lane; i < bnd[k + 1] - bnd[k]; i += RN_WAVE) {
-            sT[wid][0][bnd[k] + i] = ts[off[k] + i];
-            sI[wid][0][bnd[k] + i] = (uint16_t)(bnd[k] + i);
-        }
+    plan_stage(K, tot_r, bnd, off, ts, sT[wid][0], sI[wid][0]);
     int nr = K;
     while (true) {
         __builtin_amdgcn_wave_barrier();

@@ -128,9 +128,18 @@ struct LevelPos { uint32_t gx, gy, gz; float fx, fy, fz; };
 __device__ __forceinline__ LevelPos level_pos(float sc, float ux, float uy, float uz) {
     LevelPos p;
     float px = fmaf(sc, ux, 0.5f), py = fmaf(sc, uy, 0.5f), pz = fmaf(sc, uz, 0.5f);
-    const float ix = floorf(px), iy = floorf(py), iz = floorf(pz);
-    p.gx = (uint32_t)(int)ix; p.gy = (uint32_t)(int)iy; p.gz = (uint32_t)(int)iz;
-    p.fx = px - ix; p.fy = py - iy; p.fz = pz - iz;
+    // cell = floor, fraction = p - floor(p): v_cvt_flr_i32_f32 + v_fract_f32
+    // per axis (floor, convert and subtract took three).  p >= 0.5 (unit
+    // coordinates are clamped to [0, 1]), where p - floor(p) is exact and
+    // below 1, which is what v_fract_f32 returns
+    // (the compiler keeps floor + convert: v_cvt_flr_i32_f32 written out)
+    auto cvt_flr = [](float v) {
+        int r;
+        asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(v));
+        return (uint32_t)r;
+    };
+    p.gx = cvt_flr(px); p.gy = cvt_flr(py); p.gz = cvt_flr(pz);
+    p.fx = __builtin_amdgcn_fractf(px); p.fy = __builtin_amdgcn_fractf(py); p.fz = __builtin_amdgcn_fractf(pz);
     return p;
 }
 
