@@ -2173,8 +2173,14 @@ __device__ __forceinline__ void merge_pair_wave(const float* tA, const uint16_t*
     int a = lo, b = d - lo;
     const int e = min(d + L, n);
     for (int q = d; q < e; ++q) {
-        const bool takeA = a < nA && (b >= nB || tA[a] <= tB[b]);
-        const int idx = takeA ? iA[a] : iB[b];
+        // both heads' t and ids read together (one LDS round trip per step;
+        // as selects of the addresses, the compare, the id and the output t
+        // were three).  a = nA / b = nB read one past their run, inside the
+        // wave's slice, and are not used
+        const float ta = tA[a], tb = tB[b];
+        const int ja = iA[a], jb = iB[b];
+        const bool takeA = a < nA && (b >= nB || ta <= tb);
+        const int idx = takeA ? ja : jb;
         if (gout) {
             int base = ko[0];
 #pragma unroll
@@ -2182,7 +2188,7 @@ __device__ __forceinline__ void merge_pair_wave(const float* tA, const uint16_t*
                 if (j < K && idx >= kb[j]) base = ko[j] - kb[j];
             gout[q] = base + idx;
         } else {
-            to[q] = takeA ? tA[a] : tB[b];
+            to[q] = takeA ? ta : tb;
             io[q] = (uint16_t)idx;
         }
         a += takeA ? 1 : 0;
@@ -2195,8 +2201,9 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
                  const int32_t* __restrict__ offsets, const int32_t* __restrict__ seg_base,
                  const int32_t* __restrict__ seg_count, const float* __restrict__ ts,
                  int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
-    __shared__ float sT[PLANM_WAVES][2][PLANM_LDS];
-    __shared__ uint16_t sI[PLANM_WAVES][2][PLANM_LDS];
+    // (+2: a merge step reads one past the last run)
+    __shared__ float sT[PLANM_WAVES][2][PLANM_LDS + 2];
+    __shared__ uint16_t sI[PLANM_WAVES][2][PLANM_LDS + 2];
     static_assert(PLANM_LDS <= 65536, "u16 sample ids");
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int r = blockIdx.x * PLANM_WAVES + wid;
