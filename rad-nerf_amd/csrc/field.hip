@@ -1271,25 +1271,46 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
             const int a_k = sCh[2 + k], n_k = sCh[2 + MB_KMAX + k], roff = sCh[2 + 2 * MB_KMAX + k];
             if (n_k == 0) continue;
             uint64_t ts0 = prof ? __builtin_amdgcn_s_memtime() : 0;
-            if (k != cur_k) {
+            if (k != cur_k || !sw_ok) {
+                // model k's weights and (k != cur_k) its parked dW tiles are
+                // loaded first, then the current model's tiles are parked:
+                // vmcnt counts in issue order, so loads issued after the
+                // park's stores waited for them (a model switch took ~10 %
+                // of the MLP phase at K = 8).  A model never parked has
+                // scale 0 and its loaded tiles are dropped.
+                constexpr int WV = (FIELD_FRAGS * RN_FRAG_BYTES / 16 + BWD_WAVES * RN_WAVE - 1) /
+                                   (BWD_WAVES * RN_WAVE);
+                int4 wv[WV];
+                const int4* wsrc =
+                    reinterpret_cast<const int4*>(a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS);
+#pragma unroll
+                for (int q = 0; q < WV; ++q) {
+                    const int i = threadIdx.x + q * BWD_WAVES * RN_WAVE;
+                    wv[q] = i < FIELD_FRAGS * RN_FRAG_BYTES / 16 ? wsrc[i] : int4{0, 0, 0, 0};
+                }
+                const bool sw_k = k != cur_k;
+                const DwScale nsc = sw_k ? sScale[k] : cur;
+                f32x16 nA = accA, nB = accB;
+                if (sw_k) dw_unpark(park + (size_t)k * BWD_WAVES * 2048, nA, nB);
                 __syncthreads();                 // every wave done with sW
-                if (cur_k >= 0) {
+                if (sw_k && cur_k >= 0) {
                     dw_park(park + (size_t)cur_k * BWD_WAVES * 2048, accA, accB);
                     if (threadIdx.x == 0) sScale[cur_k] = cur;
                 }
-                rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
-                                FIELD_FRAGS * RN_FRAG_BYTES);
+                int4* wdst = reinterpret_cast<int4*>(sW);
+#pragma unroll
+                for (int q = 0; q < WV; ++q) {
+                    const int i = threadIdx.x + q * BWD_WAVES * RN_WAVE;
+                    if (i < FIELD_FRAGS * RN_FRAG_BYTES / 16) wdst[i] = wv[q];
+                }
                 __syncthreads();
-                cur = sScale[k];
-                if (cur.a != 0.f || cur.b != 0.f)
-                    dw_unpark(park + (size_t)k * BWD_WAVES * 2048, accA, accB);
-                else { accA = rn_zero16(); accB = rn_zero16(); }
-                cur_k = k;
-            } else if (!sw_ok) {                 // the walk staged its rows over sW
-                __syncthreads();
-                rn_block_copy16(sW, a.frags + (size_t)k * FIELD_FRAGS * RN_FRAG_HALFS,
-                                FIELD_FRAGS * RN_FRAG_BYTES);
-                __syncthreads();
+                if (sw_k) {
+                    cur = nsc;
+                    const bool live = nsc.a != 0.f || nsc.b != 0.f;
+                    accA = live ? nA : rn_zero16();
+                    accB = live ? nB : rn_zero16();
+                    cur_k = k;
+                }
             }
             sw_ok = true;
             if (prof) { const uint64_t t = __builtin_amdgcn_s_memtime(); cyc[4] += t - ts0; ts0 = t; }
