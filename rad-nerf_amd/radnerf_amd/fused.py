@@ -226,9 +226,11 @@ class FusedMLRenderer:
         # unpark dW, reload weights -- and ring drains per sample): C5 per GPU
         # 2048 645, 4096 664, 6144 670, 8192 671-675; C4 1024 512, 2048 533,
         # 3072 535, 4096 537, 6144 422; C3 1024 1136, 1536 1158, 2048 1148
-        # (profiles/r05/chunk3/)
+        # (profiles/r05/chunk3/); after the walk-step work of late round 5:
+        # C5 6144 728, 8192 730, 12288 734.6, 16384 734.2; C4 3072 591, 4096
+        # 589, 6144 468; C3 1024 1172, 1536 1182, 2048 1177 (profiles/r05/chunk5/)
         if model.size >= 8 and rk > 4096:
-            self.max_chunk = 8192
+            self.max_chunk = 12288
         elif model.size >= 4 and rk > 4096 and float(model.scale) > 0.5:
             self.max_chunk = 4096
         elif model.size >= 2 and rk > 4096 and float(model.scale) <= 0.5:
