@@ -138,6 +138,9 @@ def parse():
     ap.add_argument("--min-chunk", type=int, default=None,
                     help="merged backward: chunk of the last 1/8 of the work (default: the "
                          "renderer's, 512)")
+    ap.add_argument("--plan-prep", type=int, default=None,
+                    help="timing studies: 0 = the level forward's per-position input by its "
+                         "own pass instead of from rn_bwd_plan")
     ap.add_argument("--balance-chunks", type=int, default=None,
                     help="merged backward: 1 = big chunks a multiple of the persistent "
                          "blocks in number (the renderer's default), 0 = max_chunk each")
@@ -315,6 +318,8 @@ def main():
         r.level_mlp_blocks = args.mlp_blocks
     if args.balance_chunks is not None:
         r.balance_chunks = bool(args.balance_chunks)
+    if args.plan_prep is not None:
+        r.plan_prep = bool(args.plan_prep)
     ar = rdist.GradAllReduce([model.xyz_encoder.params, model.mlp_params, gate.params], dev)
     samples_acc = torch.zeros((), dtype=torch.int64, device=dev)
 

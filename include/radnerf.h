@@ -19,7 +19,7 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 7   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 8   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
@@ -212,7 +212,10 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * [cap_chunks][20] i32 = first ray, end ray, 2 pad, first sample [8], count [8]
  * per model, read by the merged kernels with one 80-B load per ticket).  cap_chunks must bound the chunk
  * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2
- * (+ balance_blocks when balancing).
+ * (+ balance_blocks when balancing).  With prep (optional, [total] x 4 f32)
+ * it also writes each merged position's (unit x, y, z, sample id as i32 bits)
+ * for rn_field_fwd_levels (then called with prep_ready = 1): rays_o, rays_d
+ * (device) and xyz_min, extent (host, 3 f32 each) are needed only then.
  * rn_field_bwd_merged runs `blocks` persistent blocks pulling chunks; each
  * stages 80-B rows in its scratch slice (scratch: blocks x scratch_rows x 20
  * f32, scratch_rows >= max_chunk + n_models * max_samples) and parks per-model
@@ -224,7 +227,9 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
                 int32_t balance_blocks, int32_t cap_chunks, int32_t* mstart, int32_t* perm,
-                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, void* stream);
+                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, const float* rays_o,
+                const float* rays_d, const float* xyz_min, const float* extent, float* prep,
+                void* stream);
 int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* rays_o,
                         const float* rays_d, const int32_t* seg_base, const int32_t* seg_count,
                         const int32_t* mstart, const int32_t* perm,
@@ -403,7 +408,8 @@ int rn_field_fwd_merged(const float* ts, const int32_t* ray_of, const float* ray
 /* Level-partitioned merged forward: the same sigma, rgb and feat_cache as
  * rn_field_fwd_merged with the merged-order encoding (bit-exact), in three
  * launches: the merged order's unit coordinates (prep: 16 B per merged
- * sample), then the encoding split by level (block b encodes levels g and
+ * sample; skipped with prep_ready != 0, when rn_bwd_plan wrote them), then
+ * the encoding split by level (block b encodes levels g and
  * 15 - g, g = b % 8, of every sample into planes[L * plane_stride + s], one
  * f16x2 per level; blocks go to the XCDs round-robin, so each XCD's L2 holds
  * two levels' tables), then the per-model MLP tiles read the planes.
@@ -420,7 +426,8 @@ int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* ray
                         const float* xyz_min, const float* extent, const void* frags,
                         float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
                         const int32_t* perm, uint32_t* planes, int64_t plane_stride, void* prep,
-                        int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq, void* stream);
+                        int32_t prep_ready, int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq,
+                        void* stream);
 
 /* ---- ray gate (networks.py:1070-1093) --------------------------------------
  * input row r = (in0[r*stride + 0..2], in1[r*stride + 0..2]): pass x (B,6)

@@ -2041,6 +2041,30 @@ k_fx_fold(int64_t e0, int64_t e1, GridMeta gm, const float* __restrict__ scale,
 // and k_bwd_plan_multi took 0.139 ms at C5).  bnd / off are wave-uniform.
 #define PLAN_UNR 8
 
+// The level-partitioned forward's per-position input (k_enc_prep's float4:
+// unit coordinates, sample id), written by the plan as it places each sample
+// (rn_bwd_plan with `prep`): the plan has the sample's t in LDS and its ray,
+// so the separate pass that re-read perm, ts and the ray (C3 0.03 ms) goes.
+// Arithmetic as load_sample<1> + unit_coord (bit-identical).
+struct PlanPrep {
+    float4* prep;             // null: the plan writes perm only
+    const float* rays_o; const float* rays_d;
+    float mn[3], ext[3];
+};
+struct RayPos { float o[3], d[3]; };
+__device__ __forceinline__ RayPos plan_ray(const PlanPrep& P, int r) {
+    RayPos q;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) { q.o[c] = P.rays_o[3 * r + c]; q.d[c] = P.rays_d[3 * r + c]; }
+    return q;
+}
+__device__ __forceinline__ void plan_prep_write(const PlanPrep& P, const RayPos& q, int pos,
+                                                float t, int s) {
+    const float x = fmaf(t, q.d[0], q.o[0]), y = fmaf(t, q.d[1], q.o[1]), z = fmaf(t, q.d[2], q.o[2]);
+    P.prep[pos] = make_float4(unit_coord(x, P.mn[0], P.ext[0]), unit_coord(y, P.mn[1], P.ext[1]),
+                              unit_coord(z, P.mn[2], P.ext[2]), __int_as_float(s));
+}
+
 // Ray r's run of each model (count, first sample) and its merged start ms.
 // r is wave-uniform (the wave id read back as a scalar), and every model's
 // words load unconditionally (index clamped to K - 1, zeroed after): scalar
@@ -2093,7 +2117,8 @@ __device__ __forceinline__ void plan_stage(int K, int tot_r, const int* bnd, con
 __global__ void __launch_bounds__(PLAN_WAVES * 64)
 k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __restrict__ offsets,
            const int32_t* __restrict__ seg_base, const int32_t* __restrict__ seg_count,
-           const float* __restrict__ ts, int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
+           const float* __restrict__ ts, int32_t* __restrict__ mstart, int32_t* __restrict__ perm,
+           PlanPrep P) {
     __shared__ float sT[PLAN_WAVES][PLAN_LDS];
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x / RN_WAVE);
     const int r = blockIdx.x * PLAN_WAVES + wid;
@@ -2114,6 +2139,7 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
     }
     const bool staged = tot_r <= PLAN_LDS;
     float* st = sT[wid];
+    const RayPos rq = P.prep ? plan_ray(P, r) : RayPos{};
     if (staged) {
         plan_stage(K, tot_r, loc, off, ts, st, nullptr);
         __builtin_amdgcn_wave_barrier();
@@ -2139,7 +2165,9 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
         const int e = min(d + L, n);
         for (int q = d; q < e; ++q) {
             const bool takeA = a < nA && (b >= nB || A[a] <= Bv[b]);
-            perm[ms + q] = takeA ? off[0] + a : off[1] + b;
+            const int smp = takeA ? off[0] + a : off[1] + b;
+            perm[ms + q] = smp;
+            if (P.prep) plan_prep_write(P, rq, ms + q, takeA ? A[a] : Bv[b], smp);
             a += takeA ? 1 : 0;
             b += takeA ? 0 : 1;
         }
@@ -2160,6 +2188,7 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
                 pos += lo;
             }
             perm[ms + pos] = off[k] + i;
+            if (P.prep) plan_prep_write(P, rq, ms + pos, t, off[k] + i);
         }
     }
 }
@@ -2181,7 +2210,8 @@ k_bwd_plan(int B, int K, const int32_t* __restrict__ counts, const int32_t* __re
 __device__ __forceinline__ void merge_pair_wave(const float* tA, const uint16_t* iA, int nA,
                                                 const float* tB, const uint16_t* iB, int nB,
                                                 float* to, uint16_t* io, int32_t* gout,
-                                                const int* kb, const int* ko, int K) {
+                                                const int* kb, const int* ko, int K,
+                                                const PlanPrep& P, const RayPos& rq, int gpos) {
     const int lane = rn_lane();
     const int n = nA + nB;
     const int L = (n + RN_WAVE - 1) / RN_WAVE;
@@ -2208,6 +2238,7 @@ __device__ __forceinline__ void merge_pair_wave(const float* tA, const uint16_t*
             for (int j = 1; j < MB_KMAX; ++j)
                 if (j < K && idx >= kb[j]) base = ko[j] - kb[j];
             gout[q] = base + idx;
+            if (P.prep) plan_prep_write(P, rq, gpos + q, takeA ? ta : tb, base + idx);
         } else {
             to[q] = takeA ? ta : tb;
             io[q] = (uint16_t)idx;
@@ -2221,7 +2252,7 @@ __global__ void __launch_bounds__(PLANM_WAVES * 64)
 k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
                  const int32_t* __restrict__ offsets, const int32_t* __restrict__ seg_base,
                  const int32_t* __restrict__ seg_count, const float* __restrict__ ts,
-                 int32_t* __restrict__ mstart, int32_t* __restrict__ perm) {
+                 int32_t* __restrict__ mstart, int32_t* __restrict__ perm, PlanPrep P) {
     // (+2: a merge step reads one past the last run)
     __shared__ float sT[PLANM_WAVES][2][PLANM_LDS + 2];
     __shared__ uint16_t sI[PLANM_WAVES][2][PLANM_LDS + 2];
@@ -2236,6 +2267,7 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
 #pragma unroll
     for (int k = 0; k < MB_KMAX; ++k) { bnd[k] = tot_r; tot_r += cnt[k]; }
     bnd[MB_KMAX] = tot_r;
+    const RayPos rq = P.prep ? plan_ray(P, r) : RayPos{};
     if (lane == 0) {
         mstart[r] = ms;
         if (r == 0) {
@@ -2262,6 +2294,7 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
                     pos += lo;
                 }
                 perm[ms + pos] = off[k] + i;
+                if (P.prep) plan_prep_write(P, rq, ms + pos, t, off[k] + i);
             }
         }
         return;
@@ -2282,7 +2315,7 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
             const int a0 = bnd[2 * p], a1 = bnd[min(2 * p + 1, nr)], b1 = bnd[min(2 * p + 2, nr)];
             merge_pair_wave(ts_ + a0, is_ + a0, a1 - a0, ts_ + a1, is_ + a1, b1 - a1,
                             sT[wid][cur ^ 1] + a0, sI[wid][cur ^ 1] + a0,
-                            last ? perm + ms + a0 : nullptr, kb, off, K);
+                            last ? perm + ms + a0 : nullptr, kb, off, K, P, rq, ms + a0);
         }
         if (last) return;
         // runs after this level: boundaries of the merged pairs
@@ -2525,19 +2558,26 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
                 const int32_t* seg_count, const float* ts, int64_t n_rays, int32_t n_models,
                 int32_t head_chunks, int32_t head_size, int32_t max_chunk, int32_t min_chunk,
                 int32_t balance_blocks, int32_t cap_chunks, int32_t* mstart, int32_t* perm,
-                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, void* stream) {
+                int32_t* chunk_first, int32_t* chunk_desc, int32_t* queue, const float* rays_o,
+                const float* rays_d, const float* xyz_min, const float* extent, float* prep,
+                void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= MB_KMAX, "bad sizes");
     RN_CHECK_ARG(max_chunk >= min_chunk && min_chunk >= 1 && cap_chunks >= 1 && head_chunks >= 0 &&
                  head_size >= 0 && head_size <= max_chunk && balance_blocks >= 0,
                  "bad chunk sizes");
     RN_CHECK_ARG(counts && offsets && seg_base && seg_count && ts && mstart && perm &&
                  chunk_first && chunk_desc && queue, "null pointer");
+    RN_CHECK_ARG(!prep || (rays_o && rays_d && xyz_min && extent), "null pointer (prep)");
+    PlanPrep P{};
+    P.prep = (float4*)prep; P.rays_o = rays_o; P.rays_d = rays_d;
+    if (prep)
+        for (int c = 0; c < 3; ++c) { P.mn[c] = xyz_min[c]; P.ext[c] = extent[c]; }
     if (n_models > 2)
         k_bwd_plan_multi<<<nblk(n_rays, PLANM_WAVES), PLANM_WAVES * 64, 0, (hipStream_t)stream>>>(
-            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
+            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm, P);
     else
         k_bwd_plan<<<nblk(n_rays, PLAN_WAVES), PLAN_WAVES * 64, 0, (hipStream_t)stream>>>(
-            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm);
+            (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm, P);
     RN_CHECK_LAUNCH();
     k_bwd_chunks<<<nblk(cap_chunks + 1, 256), 256, 0, (hipStream_t)stream>>>(
         (int)n_rays, n_models, mstart, offsets, seg_base, seg_count, head_chunks, head_size,
@@ -2720,7 +2760,8 @@ int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* ray
                         const float* xyz_min, const float* extent, const void* frags,
                         float* sigma, float* rgb, void* feat_cache, const int32_t* mstart,
                         const int32_t* perm, uint32_t* planes, int64_t plane_stride, void* prep,
-                        int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq, void* stream) {
+                        int32_t prep_ready, int32_t enc_blocks, int32_t mlp_blocks, int32_t* xq,
+                        void* stream) {
     RN_CHECK_ARG(n_rays >= 1 && n_models >= 1 && n_models <= FM_KMAX && plane_stride >= 1,
                  "bad sizes (n_models <= 8)");
     RN_CHECK_ARG(enc_blocks >= 8 && enc_blocks % 8 == 0 && mlp_blocks >= 1,
@@ -2745,7 +2786,8 @@ int rn_field_fwd_levels(const float* ts, const int32_t* ray_of, const float* ray
         rn_set_error("%s: probe reset failed", __func__);
         return 2;
     }
-    k_enc_prep<<<1024, 256, 0, st>>>(a, m, (float4*)prep);
+    // (prep_ready: rn_bwd_plan wrote the per-position input as it placed the samples)
+    if (!prep_ready) k_enc_prep<<<1024, 256, 0, st>>>(a, m, (float4*)prep);
     // level groups: (g, 15 - g) unless a study set another pairing (each level
     // exactly once: checked on the host)
     uint64_t pairing = g_level_pairing;

@@ -75,7 +75,9 @@ extern "C" {
 // 2^32 (a 24-bit multiply), fx_mode 2 refuses grids over 2^24 elements.  6
 // (round 5) rn_bwd_plan takes balance_blocks (big chunks a multiple of the
 // persistent blocks in number).  7 (round 5) wq / we weight element i by its
-// byte offset 4 i; fx_mode 2 takes grids up to 2^28 elements.
+// byte offset 4 i; fx_mode 2 takes grids up to 2^28 elements.  8 (round 5)
+// rn_bwd_plan can write the level forward's per-position input (prep),
+// rn_field_fwd_levels takes prep_ready.
 int rn_version(void) { return RN_ABI_VERSION; }
 
 const char* rn_last_error(void) { return g_err; }

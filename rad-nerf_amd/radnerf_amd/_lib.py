@@ -59,7 +59,8 @@ SIGNATURES = {
     "rn_field_fwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, I32, P],
     "rn_field_bwd": [P, P, I64, P, P, P, P, P, P, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
                      I32, P],
-    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P, P, P, P, P, P],
+    "rn_bwd_plan": [P, P, P, P, P, I64, I32, I32, I32, I32, I32, I32, I32, P, P, P, P, P,
+                    P, P, P, P, P, P],
     "rn_field_bwd_merged": [P, P, P, P, P, P, P, P, P, P, I64, I32, I32, P, P, P, P, P, P,
                             P, P, P, P, P, P, P, P, I64, P, I32, I32, P, P, P, P, P, P,
                             P, I32, P, P, P, I32, P],
@@ -80,7 +81,7 @@ SIGNATURES = {
     "rn_field_fwd_merged": [P, P, P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P,
                             P, P, I32, I32, P],
     "rn_field_fwd_levels": [P, P, P, P, P, P, I64, I32, P, P, P, P, P, P, P, P, P, P, P, P, P,
-                            P, I64, P, I32, I32, P, P],
+                            P, I64, P, I32, I32, I32, P, P],
     "rn_gate_fwd": [P, P, I32, I64, I32, P, P, P, I32, P],
     "rn_gate_bwd": [P, P, I32, I64, I32, P, P, P, I32, P, P, I32, P],
     "rn_nerf_loss": [P, P, P, P, P, P, I64, I32, F32, F32, F32, P, P, P, P, P, P],
@@ -94,7 +95,7 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 _lib = None
 
 

@@ -204,6 +204,8 @@ class FusedMLRenderer:
         # 1139, C4 401 -> 450, C5 513 -> 549 M samples/s.  Needs the plan's
         # merged order (rn_bwd_plan runs with the merged backward or forward).
         self.level_fwd = self.merged_bwd or self.merged_fwd
+        # the plan writes the level forward's per-position input (no prep pass)
+        self.plan_prep = True
         self.level_enc_blocks = 4096
         self.level_mlp_blocks = 256
         self.merged_blocks = 256
@@ -387,7 +389,8 @@ class FusedMLRenderer:
                  MAX_SAMPLES, w.stage_ts.data_ptr(), w.stage_dt.data_ptr(), w.ts.data_ptr(),
                  w.deltas.data_ptr(), w.ray_of.data_ptr(), st)
         if self.merged_bwd or self.merged_fwd:
-            self._plan(st)
+            # the plan also writes the level forward's per-position input
+            self._plan(st, rays_o, rays_d if self.level_fwd and self.plan_prep else None)
         self._field(True, rays_o, rays_d, st)
         self._ev("composite_fw", L.ml_composite_fw, w.sigma.data_ptr(), w.rgb.data_ptr(), w.deltas.data_ptr(),
                           w.ts.data_ptr(), w.counts.data_ptr(), w.offsets.data_ptr(), B, K,
@@ -421,10 +424,13 @@ class FusedMLRenderer:
         """Columns of a (B, G) per-ray tensor that belong to the rendered sub-NeRFs."""
         return x
 
-    def _plan(self, st):
+    def _plan(self, st, rays_o=None, rays_d=None):
         """Merged (ray, t) order + chunk schedule of this step's samples
-        (rn_bwd_plan), shared by the merged forward and backward."""
-        w, L = self.ws, lib()
+        (rn_bwd_plan), shared by the merged forward and backward; with the
+        rays (forward, level-partitioned encode) also the encode's
+        per-position input, so rn_field_fwd_levels skips its prep pass."""
+        w, L, m = self.ws, lib(), self.model
+        prep = w.level_buffers(st)[1] if rays_d is not None else None
         self._min_chunk = min(self.min_chunk, self.max_chunk)
         head_n = self.merged_blocks if self.head_chunk else 0
         head = min(self.head_chunk, self.max_chunk)
@@ -434,8 +440,14 @@ class FusedMLRenderer:
                  w.seg_base.data_ptr(), w.seg_count.data_ptr(), w.ts.data_ptr(), w.B, w.K,
                  head_n, head, self.max_chunk, self._min_chunk, bal, self._cap_chunks,
                  w.mstart.data_ptr(), w.perm.data_ptr(), self._chunks.data_ptr(),
-                 w._chunk_desc.data_ptr(), w.queue.data_ptr(), st)
+                 w._chunk_desc.data_ptr(), w.queue.data_ptr(),
+                 None if prep is None else rays_o.data_ptr(),
+                 None if prep is None else rays_d.data_ptr(),
+                 None if prep is None else m._h_min.ctypes.data,
+                 None if prep is None else m._h_ext.ctypes.data,
+                 None if prep is None else prep.data_ptr(), st)
         self._plan_key = (self.max_chunk, self._min_chunk, head_n, head, bal)
+        self._prep_ready = prep is not None
 
     def _field(self, fwd, rays_o, rays_d, st, grid_grad=None, dw=None):
         m, w, L = self.model, self.ws, lib()
@@ -450,8 +462,10 @@ class FusedMLRenderer:
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),
                      w.seg_count.data_ptr(), w.B, m.size, *common[10:], w.sigma.data_ptr(),
                      w.rgb.data_ptr(), w.feat.data_ptr(), w.mstart.data_ptr(), w.perm.data_ptr(),
-                     planes.data_ptr(), planes.shape[1], prep.data_ptr(), self.level_enc_blocks,
+                     planes.data_ptr(), planes.shape[1], prep.data_ptr(),
+                     int(getattr(self, "_prep_ready", False)), self.level_enc_blocks,
                      self.level_mlp_blocks, None, st)
+            self._prep_ready = False
         elif fwd and self.merged_fwd:
             self._ev("field_fwd", L.field_fwd_merged, w.ts.data_ptr(), w.ray_of.data_ptr(),
                      rays_o.data_ptr(), rays_d.data_ptr(), w.seg_base.data_ptr(),

@@ -590,3 +590,28 @@ def test_fused_mostly_empty_rays(cuda, K):
     for a, b in zip(gf, gd):
         rel = (a - b).norm() / b.norm().clamp_min(1e-30)
         assert rel <= 1e-3, rel
+
+
+@pytest.mark.parametrize("B,K,scale", [(2048, 2, 0.5), (1024, 8, 16.0), (512, 1, 0.5)])
+def test_plan_writes_level_forward_input(cuda, B, K, scale):
+    """rn_bwd_plan with `prep` writes the level forward's per-position input
+    (unit coordinates, sample id) as it places each sample; bit-identical to
+    the separate prep pass of rn_field_fwd_levels (K = 2: the two-run merge;
+    K = 8: the merge tree; K = 1: the rank path)."""
+    esf = 1 / 256 if scale > 0.5 else 0.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    to = lambda a: torch.from_numpy(a).to(cuda)
+    preps = []
+    for pp in (False, True):
+        r.plan_prep, r.level_fwd = pp, True
+        ml_render_fused(m, g, to(o), to(d), to(d), noise=to(noise), exp_step_factor=esf)
+        torch.cuda.synchronize()
+        w = r.ws
+        total = int(w.mstart[B])
+        prep = w.level_buffers(torch.cuda.current_stream().cuda_stream)[1]
+        preps.append(prep[:total].clone())
+        prep.fill_(float("nan"))
+    r.plan_prep = True
+    assert preps[0].shape[0] > 0
+    assert torch.equal(preps[0].view(torch.int32), preps[1].view(torch.int32))

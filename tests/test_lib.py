@@ -61,10 +61,10 @@ def test_arg_validation_without_gpu():
     # level-partitioned forward: level groups come in eights, at most 8 sub-NeRFs
     lv = [None] * 6 + [8, 2] + [None] * 14 + [16, None]
     with pytest.raises(RuntimeError, match="rn_field_fwd_levels.*multiple of 8"):
-        L.field_fwd_levels(*lv, 12, 1, None, None)
+        L.field_fwd_levels(*lv, 0, 12, 1, None, None)
     lv[7] = 9
     with pytest.raises(RuntimeError, match="rn_field_fwd_levels.*n_models <= 8"):
-        L.field_fwd_levels(*lv, 16, 1, None, None)
+        L.field_fwd_levels(*lv, 0, 16, 1, None, None)
     # a level pairing must name every level exactly once
     with pytest.raises(RuntimeError, match="every level exactly once"):
         L.set_level_pairing(0x11)

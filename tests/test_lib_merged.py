@@ -13,11 +13,11 @@ def test_merged_entry_points_validate_without_gpu():
     L = _lib.lib()
     P = [None] * 32
     with pytest.raises(RuntimeError, match="bad chunk sizes"):
-        L.bwd_plan(*P[:5], 8, 2, 0, 0, 256, 512, 0, 10, *P[:6])
+        L.bwd_plan(*P[:5], 8, 2, 0, 0, 256, 512, 0, 10, *P[:11])
     with pytest.raises(RuntimeError, match="bad chunk sizes"):
-        L.bwd_plan(*P[:5], 8, 2, 0, 0, 1024, 512, -1, 10, *P[:6])
+        L.bwd_plan(*P[:5], 8, 2, 0, 0, 1024, 512, -1, 10, *P[:11])
     with pytest.raises(RuntimeError, match="rn_bwd_plan: bad sizes"):
-        L.bwd_plan(*P[:5], 8, 9, 0, 0, 1024, 512, 0, 10, *P[:6])
+        L.bwd_plan(*P[:5], 8, 9, 0, 0, 1024, 512, 0, 10, *P[:11])
     with pytest.raises(RuntimeError, match="n_models <= 8"):
         L.field_fwd_merged(*P[:8], 8, 9, *P[:13], 256, 512, None)
     with pytest.raises(RuntimeError, match="threads"):

@@ -55,7 +55,7 @@ def main():
                            m.packed_frags().data_ptr(), w.sigma.data_ptr(), w.rgb.data_ptr(),
                            w.feat.data_ptr() if feat else None, w.mstart.data_ptr(),
                            w.perm.data_ptr(),
-                           planes.data_ptr(), stride, prep.data_ptr(), eb, mb,
+                           planes.data_ptr(), stride, prep.data_ptr(), 0, eb, mb,
                            xq.data_ptr() if probe else None, st)
 
     def timed(fn):
