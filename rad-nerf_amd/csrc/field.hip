@@ -2050,6 +2050,10 @@ struct PlanPrep {
     float4* prep;             // null: the plan writes perm only
     const float* rays_o; const float* rays_d;
     float mn[3], ext[3];
+    // 1 / extent when every extent is a power of two (scale 0.5: 1, scale 16:
+    // 32): x / ext and x * (1 / ext) are then the same float, and the three
+    // IEEE divisions per sample leave the merge's serial chain; 0 otherwise
+    float inv[3];
 };
 struct RayPos { float o[3], d[3]; };
 __device__ __forceinline__ RayPos plan_ray(const PlanPrep& P, int r) {
@@ -2061,8 +2065,11 @@ __device__ __forceinline__ RayPos plan_ray(const PlanPrep& P, int r) {
 __device__ __forceinline__ void plan_prep_write(const PlanPrep& P, const RayPos& q, int pos,
                                                 float t, int s) {
     const float x = fmaf(t, q.d[0], q.o[0]), y = fmaf(t, q.d[1], q.o[1]), z = fmaf(t, q.d[2], q.o[2]);
-    P.prep[pos] = make_float4(unit_coord(x, P.mn[0], P.ext[0]), unit_coord(y, P.mn[1], P.ext[1]),
-                              unit_coord(z, P.mn[2], P.ext[2]), __int_as_float(s));
+    auto u = [&](float v, int c) {
+        return P.inv[0] != 0.f ? fminf(fmaxf((v - P.mn[c]) * P.inv[c], 0.0f), 1.0f)
+                               : unit_coord(v, P.mn[c], P.ext[c]);
+    };
+    P.prep[pos] = make_float4(u(x, 0), u(y, 1), u(z, 2), __int_as_float(s));
 }
 
 // Ray r's run of each model (count, first sample) and its merged start ms.
@@ -2570,8 +2577,16 @@ int rn_bwd_plan(const int32_t* counts, const int32_t* offsets, const int32_t* se
     RN_CHECK_ARG(!prep || (rays_o && rays_d && xyz_min && extent), "null pointer (prep)");
     PlanPrep P{};
     P.prep = (float4*)prep; P.rays_o = rays_o; P.rays_d = rays_d;
-    if (prep)
-        for (int c = 0; c < 3; ++c) { P.mn[c] = xyz_min[c]; P.ext[c] = extent[c]; }
+    if (prep) {
+        bool pow2 = true;
+        for (int c = 0; c < 3; ++c) {
+            P.mn[c] = xyz_min[c]; P.ext[c] = extent[c];
+            int e;
+            pow2 = pow2 && extent[c] > 0.f && std::frexp(extent[c], &e) == 0.5f &&
+                   e > -120 && e < 120;
+        }
+        for (int c = 0; c < 3; ++c) P.inv[c] = pow2 ? 1.0f / extent[c] : 0.f;
+    }
     if (n_models > 2)
         k_bwd_plan_multi<<<nblk(n_rays, PLANM_WAVES), PLANM_WAVES * 64, 0, (hipStream_t)stream>>>(
             (int)n_rays, n_models, counts, offsets, seg_base, seg_count, ts, mstart, perm, P);
