@@ -272,7 +272,8 @@ class FusedMLRenderer:
         self.bin_records_per_pair = 6912
         self.min_chunk = 512
         # optional short first chunk per block (starts the scatter sooner):
-        # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms)
+        # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms); round 5
+        # again: C3 1185-1187 and C5 732-736 at 0-512 (profiles/r05/chunk5/)
         self.head_chunk = 0
         # big chunks a multiple of the persistent blocks in number (rn_bwd_plan
         # balance_blocks): every block takes the same number of them
