@@ -2322,9 +2322,28 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
             const int a0 = bnd[2 * p], a1 = bnd[min(2 * p + 1, nr)], b1 = bnd[min(2 * p + 2, nr)];
             merge_pair_wave(ts_ + a0, is_ + a0, a1 - a0, ts_ + a1, is_ + a1, b1 - a1,
                             sT[wid][cur ^ 1] + a0, sI[wid][cur ^ 1] + a0,
-                            last ? perm + ms + a0 : nullptr, kb, off, K, P, rq, ms + a0);
+                            nullptr, kb, off, K, P, rq, ms + a0);
         }
-        if (last) return;
+        if (last) {
+            // the merged order is in LDS like every level's: perm (and the
+            // level forward's input) go out in position order, coalesced and
+            // off the merge's serial chain (written from inside it, each
+            // lane's stores were L positions apart)
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            const float* to = sT[wid][cur ^ 1];
+            const uint16_t* io = sI[wid][cur ^ 1];
+            for (int q = lane; q < tot_r; q += RN_WAVE) {
+                const int idx = io[q];
+                int base = off[0];
+#pragma unroll
+                for (int jk = 1; jk < MB_KMAX; ++jk)
+                    if (jk < K && idx >= kb[jk]) base = off[jk] - kb[jk];
+                perm[ms + q] = base + idx;
+                if (P.prep) plan_prep_write(P, rq, ms + q, to[q], base + idx);
+            }
+            return;
+        }
         // runs after this level: boundaries of the merged pairs
         const int nn = (nr + 1) / 2;
         for (int p = 0; p < nn; ++p) bnd[p] = bnd[2 * p];
