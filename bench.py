@@ -159,7 +159,7 @@ def parse():
     ap.add_argument("--buckets", type=int, default=4,
                     help="N>1: the gradient all-reduce as this many asynchronous bucket "
                          "collectives, each averaged behind its own wait (1 = one collective)")
-    ap.add_argument("--grid-split", type=int, default=8,
+    ap.add_argument("--grid-split", type=int, default=8, choices=range(16), metavar="[0-15]",
                     help="N>1, binned fold: the grid levels [this, 16) are summed first and "
                          "their all-reduce starts while levels [0, this) are summed")
     ap.add_argument("--launch-check", action="store_true",
@@ -230,11 +230,21 @@ def launch_check(args, rank, local, world):
         for h in hs:
             ar.finish(h)
         comm = ar.comm_stats(1)
-        # the same local gradients through one plain all-reduce: bit-identical
+        # the same local gradients through one plain all-reduce: equal within
+        # rounding (bit-identical at world 2; with more ranks the ring's
+        # summation order follows the bucket bounds), and the same bits on
+        # every rank
         ref = local.clone()
         dist.all_reduce(ref)
         ref.div_(world)
-        comm["mean_ok"] = bool(torch.equal(ar.flat, ref))
+        r0 = ar.flat.clone()
+        dist.broadcast(r0, 0)
+        same = torch.tensor([int(torch.equal(ar.flat, r0))])
+        dist.all_reduce(same, op=dist.ReduceOp.MIN)
+        comm["mean_bit_identical"] = bool(torch.equal(ar.flat, ref))
+        comm["rank_consistent"] = bool(same.item())
+        comm["mean_ok"] = bool(torch.allclose(ar.flat, ref, rtol=1e-6, atol=1e-6)) \
+            and comm["rank_consistent"]
         comm["ranges"] = {k: list(v) for k, v in rg.items()}
         comm["backend"] = dist.get_backend()
     if rank == 0:

@@ -13,10 +13,18 @@ kernel produces the same grids.  `broadcast_buffers` (rank 0's copy, C x 256
 KiB per sub-NeRF) remains for callers that update with torch's default
 stream.
 """
+import datetime
 import os
 
 import torch
 import torch.distributed as dist
+
+# a collective that has not completed after this many seconds fails the rank
+# (VERDICT r05 item 4): torch's default is 10 min for RCCL / 30 min for gloo,
+# longer than the driver gives a bench run, so a hung all-reduce would run to
+# the driver's limit instead of exiting non-zero.  RADNERF_DIST_TIMEOUT
+# overrides it (seconds).
+DEFAULT_TIMEOUT_S = 300
 
 
 def env_rank():
@@ -31,20 +39,50 @@ def device_index(local):
     return int(pinned) if pinned is not None else local
 
 
-def init(backend=None):
-    """Initialise the default process group from the torchrun env (no-op for 1 rank)."""
+def collective_timeout(timeout_s=None):
+    """The process group's collective timeout: timeout_s, else
+    $RADNERF_DIST_TIMEOUT, else DEFAULT_TIMEOUT_S seconds."""
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("RADNERF_DIST_TIMEOUT", DEFAULT_TIMEOUT_S))
+    return datetime.timedelta(seconds=float(timeout_s))
+
+
+def init(backend=None, timeout_s=None):
+    """Initialise the default process group from the torchrun env (no-op for 1
+    rank), with a bounded collective timeout (collective_timeout).  Under RCCL
+    a collective past it is caught by torch's watchdog, which aborts the
+    communicator and ends the rank non-zero with the operation's sequence
+    number and size in its message (TORCH_NCCL_ASYNC_ERROR_HANDLING's default
+    teardown); under gloo the wait raises, and GradAllReduce re-raises it with
+    the rank and bucket (CollectiveTimeout)."""
     rank, local, world = env_rank()
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
+        timeout = collective_timeout(timeout_s)
         if backend == "nccl":
             dev = device_index(local)
             torch.cuda.set_device(dev)
-            dist.init_process_group(backend, device_id=torch.device("cuda", dev))
+            dist.init_process_group(backend, device_id=torch.device("cuda", dev), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     return rank, local, world
+
+
+class CollectiveTimeout(RuntimeError):
+    """A bucket's collective failed or did not complete in time; the message
+    names the rank, the bucket and its range of the flat buffer."""
+
+
+def _wait(work, what):
+    """work.wait(), re-raising a failure with the rank and bucket `what`."""
+    try:
+        work.wait()
+    except Exception as e:
+        rank = dist.get_rank() if dist.is_initialized() else 0
+        raise CollectiveTimeout(f"rank {rank}: {what} did not complete "
+                                f"({type(e).__name__}: {str(e)[:300]})") from e
 
 
 def shard_rays(n_total, rank, world):
@@ -168,8 +206,8 @@ class GradAllReduce:
         else:
             import time
             parts = []
-            for rng, w, t0 in handle["parts"]:
-                w.wait()
+            for i, (rng, w, t0) in enumerate(handle["parts"]):
+                _wait(w, f"all-reduce bucket {i} [{rng[0]}, {rng[1]}) of {self.flat.numel()}")
                 parts.append((rng, t0, time.perf_counter()))
             handle["parts"] = parts
         if average:
@@ -212,8 +250,8 @@ class GradAllReduce:
         over ranks (average) or the sum."""
         if dist.is_initialized() and dist.get_world_size() > 1:
             world = dist.get_world_size()
-            for (a, b), w in self._launch(n_buckets):
-                w.wait()
+            for i, ((a, b), w) in enumerate(self._launch(n_buckets)):
+                _wait(w, f"all-reduce bucket {i} [{a}, {b}) of {self.flat.numel()}")
                 if average:
                     self.flat[a:b].div_(world)
         return self.views
@@ -239,8 +277,8 @@ class GradAllReduce:
         for p in self.params:
             offs.append(off)
             off += p.numel()
-        for (a, b), w in works:
-            w.wait()
+        for i, ((a, b), w) in enumerate(works):
+            _wait(w, f"all-reduce bucket {i} [{a}, {b}) of {self.flat.numel()} (Adam epilogue)")
             if average:
                 self.flat[a:b].div_(world)
             for p, o in zip(self.params, offs):
@@ -261,10 +299,14 @@ def step_ranges(ar, level_offset, split_level):
                summed them (FusedMLRenderer.after_grid_levels), so their
                collective overlaps the coarse levels' sum pass;
       "coarse" levels [0, split_level) after the fold.
-    split_level 0: "fine" is the whole grid and "coarse" empty.  The three
+    split_level 0: "fine" is the whole grid and "coarse" empty.  The level
+    is clamped to [0, 15] as the renderer clamps it (fused.clamp_split): a
+    cut at 16 would release the grid before any level is summed.  The three
     ranges tile the flat buffer (tests/test_dist.py)."""
+    from .fused import clamp_split
+    split_level = clamp_split(split_level)
     g0, g1 = ar.param_range(0, 1)
-    cut = g0 + 2 * int(level_offset[split_level]) if 0 < split_level < 16 else g0
+    cut = g0 + 2 * int(level_offset[split_level]) if split_level > 0 else g0
     return {"rest": ar.param_range(1), "fine": (cut, g1), "coarse": (g0, cut)}
 
 

@@ -26,6 +26,15 @@ SEG_ALIGN = 128
 FX_STATS_BYTES = 640      # include/radnerf.h RN_FX_STATS_BYTES
 
 
+def clamp_split(split_level):
+    """The binned fold's level cut for the data-parallel hook schedule, in
+    [0, 15]: levels [cut, 16) are summed first and handed to
+    after_grid_levels, then [0, cut).  0 sums the whole grid at once; 16
+    would leave the first sum empty and release the grid before any level
+    was summed, so it is clamped to 15."""
+    return max(0, min(15, int(split_level)))
+
+
 def _stream(dev):
     return torch.cuda.current_stream(dev).cuda_stream
 
@@ -562,7 +571,9 @@ class FusedMLRenderer:
                 seen[1].record(torch.cuda.current_stream(grid_grad.device))
                 fx_redo()
                 span = self._ev_open("fx_sum")
-                split = max(0, min(16, int(self.grid_split_level))) if self.after_grid_levels else 0
+                # a split of 16 would hand the whole grid over before any level
+                # is summed: the cut lies in [0, 15]
+                split = clamp_split(self.grid_split_level) if self.after_grid_levels else 0
                 sums = ((split, 16), (0, split)) if split > 0 else ((0, 16),)
                 for i, (l0, l1) in enumerate(sums):
                     L.grid_sum(lo, lh, pool["ctl"].data_ptr(), pool["desc"].data_ptr(),
@@ -584,11 +595,13 @@ class FusedMLRenderer:
                 if self.after_grid_levels is not None:
                     self.after_grid_levels(0)
                 w.fx_i ^= 1
-            elif self.after_grid_levels is not None:
-                self.after_grid_levels(0)             # fp32 atomics: final after field_bwd
             if self.int_grad:
                 self._ev("igrad_to_f32", L.igrad_to_f32, grid_grad.numel(), ig[0], ig[1], ig[2],
                          grid_grad.data_ptr(), st)
+            if not (use_bin or use_fx) and self.after_grid_levels is not None:
+                # fp32 atomics: final after field_bwd (int_grad: after its
+                # conversion into grid_grad)
+                self.after_grid_levels(0)
         else:
             self._ev("field_bwd", L.field_bwd, *common, w.dsigma.data_ptr(),
                      w.drgb.data_ptr(), grid_grad.data_ptr(), dw.data_ptr(),

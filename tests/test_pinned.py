@@ -46,13 +46,14 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, K=4, scale=0.5):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     try:
+        torch.set_num_threads(1)
         rdist.init(backend="gloo")
-        K, B = 4, 16
-        m = MNGP(0.5, size=K, seed=3)
+        B = 16
+        m = MNGP(scale, size=K, seed=3)
         g = Ray_Gate(K, seed=4)
         r = PinnedMLRenderer(m, g, B, device=torch.device("cpu"))
         k0, k1 = r.k0, r.k1
@@ -99,3 +100,23 @@ def test_pinned_exchange_gloo_world2():
     assert res[0][1] == (0, 2) and res[1][1] == (2, 4), res
     assert all(r[2] and r[3] and r[4] for r in res), res
     assert [r[5] for r in res] == [True, False], res
+
+
+def test_pinned_exchange_gloo_world8_c5():
+    """C5's layout (Free / road, K = 8 on 8 GPUs, scale 16): 8 gloo ranks, one
+    sub-NeRF each -- every rank gathers all 8 sub-NeRFs' per-ray outputs in
+    model order, takes its own (B, 1) gate column, the grid partials sum over
+    the 8 ranks, each MLP row comes from its owner only and the gate gradient
+    from rank 0 only."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 8, port, q, 8, 16.0)) for r in range(8)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert [r[1] for r in res] == [(k, k + 1) for k in range(8)], res
+    assert all(r[2] and r[3] and r[4] for r in res), res
+    assert [r[5] for r in res] == [True] + [False] * 7, res
