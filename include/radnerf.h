@@ -19,10 +19,16 @@
 extern "C" {
 #endif
 
-#define RN_ABI_VERSION 8   /* rn_version(): bumped on every incompatible ABI change */
+#define RN_ABI_VERSION 9   /* rn_version(): bumped on every incompatible ABI change */
 #define RN_FX_STATS_BYTES 640   /* the fx_stats block of rn_field_bwd_merged / rn_grid_fx_fold */
 int rn_version(void);
 const char* rn_last_error(void);
+/* the signature of every rn_* entry of this header, as the library was built:
+ * "name:codes;..." with one code per parameter (p pointer, i int32, l int64,
+ * u uint64, f float, d double), generated from this file at build time
+ * (csrc/gen_sig.py).  A binding compares it with its own argument lists and
+ * refuses a library built from another revision of the header. */
+const char* rn_abi_signatures(void);
 /* ablation switches for kernel studies (tools/ablate.py); 0 = production */
 void rn_set_debug_flags(int flags);
 /* ablation builds (debug flag 4096): per-phase wave cycles of the merged
@@ -211,8 +217,10 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * queue [3] i32 = bwd ticket, chunk count, fwd ticket; chunk_desc
  * [cap_chunks][20] i32 = first ray, end ray, 2 pad, first sample [8], count [8]
  * per model, read by the merged kernels with one 80-B load per ticket).  cap_chunks must bound the chunk
- * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + 2
- * (+ balance_blocks when balancing).  With prep (optional, [total] x 4 f32)
+ * count: >= head_chunks + total/max_chunk + total/(8*min_chunk) + max_chunk/min_chunk + 3
+ * (+ balance_blocks when balancing): the last big chunk can leave up to
+ * max_chunk more samples to the min_chunk tail.  A smaller cap
+ * truncates the schedule: the samples past it are not scattered.  With prep (optional, [total] x 4 f32)
  * it also writes each merged position's (unit x, y, z, sample id as i32 bits)
  * for rn_field_fwd_levels (then called with prep_ready = 1): rays_o, rays_d
  * (device) and xyz_min, extent (host, 3 f32 each) are needed only then.

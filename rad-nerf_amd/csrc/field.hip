@@ -1923,10 +1923,17 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 // units (2^3 of headroom for growth; the first step's entries are read from
 // the fp32 grid_grad); a dense level with no entry measured maps its largest
 // record to < 2^14 units.
+#ifndef FX_TARGET_BITS              // (-D overrides: unit studies, tools/fx_units_probe.py)
 #define FX_TARGET_BITS 23
+#endif
+#ifndef FX_ENTRY_BITS
 #define FX_ENTRY_BITS 28
+#endif
 #define FX_DENSE_FIRST_BITS 14
-#define FX_GROWTH_UNITS 268435456.f       // 2^28
+#ifndef FX_GROWTH_BITS
+#define FX_GROWTH_BITS 28
+#endif
+#define FX_GROWTH_UNITS ((float)(1u << FX_GROWTH_BITS))   // 2^28
 // Binned mode (ctl != NULL, rn_grid_binned_fold): records are e5m17 (rn_bin.h),
 // summed exactly in int64, so there is no entry cap and no wrap check; the
 // largest record maps to < 2^GB_TARGET_BITS = 2^38 units (256x headroom below
@@ -2689,7 +2696,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
     }
     if (fx_mode == 4) {
-        if (hipMemsetAsync(gb_ctl, 0, sizeof(GbCtl), st) != hipSuccess) {
+        if (hipMemsetAsync(gb_ctl, 0, GB_CTL_RESET_BYTES, st) != hipSuccess) {
             rn_set_error("%s: page pool reset failed", __func__);
             return 2;
         }

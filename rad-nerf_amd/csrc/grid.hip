@@ -3,6 +3,7 @@
 // Reference: models/csrc/raymarching.cu:62-161 (morton3D, morton3D_invert,
 // packbits), used by MNGP.update_density_grid (models/networks.py:330-409).
 #include "rn_common.h"
+#include "rn_sig.h"
 #include <stdarg.h>
 #include <stdio.h>
 #pragma clang fp contract(off)
@@ -77,8 +78,11 @@ extern "C" {
 // persistent blocks in number).  7 (round 5) wq / we weight element i by its
 // byte offset 4 i; fx_mode 2 takes grids up to 2^28 elements.  8 (round 5)
 // rn_bwd_plan can write the level forward's per-position input (prep),
-// rn_field_fwd_levels takes prep_ready.
+// rn_field_fwd_levels takes prep_ready.  9 (round 6) rn_abi_signatures: the
+// per-entry signature table, checked by the binding at load.
 int rn_version(void) { return RN_ABI_VERSION; }
+
+const char* rn_abi_signatures(void) { return RN_SIGNATURE_TABLE; }
 
 const char* rn_last_error(void) { return g_err; }
 

@@ -14,6 +14,7 @@
 // Reference: the tcnn hash-grid backward this replaces
 // (/root/reference/models/networks.py:300-328 -> tinycudann GridEncoding).
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 
 #define GB_PAGE 8192              // records per page (64 KB)
@@ -54,8 +55,12 @@ __host__ __device__ __forceinline__ uint32_t gb_slice_bits(uint32_t hsize) {
 // steps differed from fp32's by 24 % per level; an e4m18 form (unit 2^-27)
 // still flushed 0.05 % (4.8 %), all of them entries below half a unit
 // (tools/fx_entry_diag.py).  The sum pass adds m << e
-// exactly in int64 (an entry would need 2^25 records at the growth bound to
-// overflow), so the sums stay order-free and bitwise reproducible.
+// exactly in int64, so the sums stay order-free and bitwise reproducible.
+// Overflow margin: a record can reach just under 2^46 units
+// before the step is flagged for the redo, so an entry would need ~2^17 such
+// records to leave int64 (2^25 at the 2^38 target that scales aim for); a
+// scale-16 step puts tens of records on an entry, a coarse dense entry a few
+// thousand.
 __host__ __device__ __forceinline__ uint32_t gb_encode(float x) {
     const uint32_t E = (__builtin_bit_cast(uint32_t, x) >> 23) & 0xffu;   // biased exponent
     int e = (int)E - (127 + 14);
@@ -109,8 +114,18 @@ struct GbCtl {
     uint32_t pool_next;           // pages taken by the walk (may exceed the pool: overflow)
     uint32_t level_npages[16];    // pages of each level (the bin pass fills level_pages)
     uint32_t fault;               // GB_FAULT_* bits: inputs the passes refused (-> redo)
-    uint32_t pad[14];
+    // sticky: GB_FAULT_RUN bits of every sum pass since the block was created
+    // (the per-step reset stops before it, GB_CTL_RESET_BYTES).  The sum pass
+    // runs after the step's check and redo launch, so a run it refuses cannot
+    // redo that step any more; the renderer reads this word back with the page
+    // count and raises, instead of applying a partial gradient
+    // unnoticed.
+    uint32_t sum_fault;
+    uint32_t pad[13];
 };
+#define GB_CTL_RESET_BYTES (18 * 4)      // pool_next, level_npages[16], fault
+static_assert(offsetof(GbCtl, sum_fault) == GB_CTL_RESET_BYTES, "GbCtl reset span");
+static_assert(sizeof(GbCtl) == 128, "GbCtl is 128 B (rn_grid_bin_layout ctl_bytes)");
 // fault bits: a page's meta names a level >= 16 or more than GB_PAGE records
 // (bin pass); a record's entry index lies outside its level (bin pass); a
 // level's page list overflowed the pool (bin pass); a page id or run outside

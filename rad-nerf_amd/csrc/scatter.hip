@@ -284,6 +284,7 @@ k_grid_sum(GbPool P, GbSumArgs s, const float* __restrict__ scale, const int32_t
                 d = pg_ok ? P.desc[(size_t)pg * GB_MAX_BINS + b] : 0u;
                 if (!pg_ok || (d & 0xffffu) + (d >> 16) > GB_PAGE) {
                     atomicOr(&P.ctl->fault, GB_FAULT_RUN);
+                    atomicOr(&P.ctl->sum_fault, GB_FAULT_RUN);     // sticky: read by the host
                     pg = 0u; d = 0u;
                 }
             }

@@ -95,8 +95,21 @@ SIGNATURES = {
     "rn_scatter_max": [P, P, I64, P, P],
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 _lib = None
+
+_CODE = {P: "p", I32: "i", I64: "l", F32: "f", F64: "d", U64: "u"}
+
+
+def binding_signatures():
+    """SIGNATURES in the library's table format (csrc/gen_sig.py): name ->
+    one code per parameter."""
+    return {n: "".join(_CODE[t] for t in a) for n, a in SIGNATURES.items()}
+
+
+def parse_signature_table(text):
+    """rn_abi_signatures()'s "name:codes;..." -> {name: codes}."""
+    return dict(e.split(":", 1) for e in text.split(";") if e)
 
 
 class _Checked:
@@ -130,8 +143,32 @@ class _Lib:
         self.handle.rn_set_debug_flags.restype = None
         self.set_debug_flags = self.handle.rn_set_debug_flags
         self.path = path
+        # the ABI checks come before any entry is bound: a library of another
+        # revision is refused here, never called with shifted arguments
+        self.check_version()
+        self.check_signatures()
         for name in SIGNATURES:
             setattr(self, name[3:], _Checked(self.handle, name))
+
+    def check_signatures(self):
+        """Compare the library's own signature table (rn_abi_signatures,
+        generated from the header it was built with) with SIGNATURES, entry by
+        entry; ImportError naming every entry that differs or is missing."""
+        try:
+            fn = self.handle.rn_abi_signatures
+        except AttributeError:
+            raise ImportError(f"radnerf_amd: {self.path} exports no rn_abi_signatures "
+                              f"(built before ABI 9); rebuild with `make -C rad-nerf_amd/csrc`")
+        fn.restype, fn.argtypes = ctypes.c_char_p, []
+        have = parse_signature_table(fn().decode())
+        bad = []
+        for name, codes in binding_signatures().items():
+            if have.get(name) != codes:
+                bad.append(f"{name}: library {have.get(name, 'missing')!s} vs binding {codes}")
+        if bad:
+            raise ImportError(f"radnerf_amd: {self.path} was built from another revision of "
+                              f"include/radnerf.h ({len(bad)} entr{'y' if len(bad) == 1 else 'ies'}"
+                              f" differ): " + "; ".join(bad[:8]))
 
     def version(self):
         return self.handle.rn_version()
@@ -159,7 +196,6 @@ def lib():
     global _lib
     if _lib is None:
         _lib = _Lib(LIB_PATH)
-        _lib.check_version()
     return _lib
 
 
@@ -174,4 +210,5 @@ def use_ablation_build():
 
 
 def exported_symbols():
-    return ["rn_version", "rn_last_error", "rn_set_debug_flags"] + list(SIGNATURES)
+    return ["rn_version", "rn_last_error", "rn_set_debug_flags",
+            "rn_abi_signatures"] + list(SIGNATURES)

@@ -26,6 +26,12 @@ SEG_ALIGN = 128
 FX_STATS_BYTES = 640      # include/radnerf.h RN_FX_STATS_BYTES
 
 
+# GbCtl (csrc/rn_bin.h) words read back after each binned backward: pool_next
+# (word 0) ... sum_fault (word 18, sticky across steps)
+GB_SUM_FAULT = 18
+GB_CTL_READ = GB_SUM_FAULT + 1
+
+
 def clamp_split(split_level):
     """The binned fold's level cut for the data-parallel hook schedule, in
     [0, 15]: levels [cut, 16) are summed first and handed to
@@ -84,8 +90,10 @@ class Workspace:
 
     def chunk_list(self, max_chunk, min_chunk, head_chunks=0, balance_blocks=0):
         """rn_bwd_plan's chunk list, sized for the workspace capacity."""
-        cap = (head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) + 2 +
-               balance_blocks)
+        # include/radnerf.h's bound (the tail after the last big chunk can
+        # hold up to max_chunk more samples in min_chunk pieces, ADVICE r05)
+        cap = (head_chunks + self.capacity // max_chunk + self.capacity // (8 * min_chunk) +
+               max_chunk // min_chunk + 3 + balance_blocks)
         if self._chunks is None or self._chunks.numel() < cap + 1:
             self._chunks = torch.empty(cap + 1, device=self.device, dtype=torch.int32)
             self._chunk_desc = torch.empty(cap + 1, 20, device=self.device, dtype=torch.int32)
@@ -567,7 +575,8 @@ class FusedMLRenderer:
                 # the pages this backward took, read back without a sync
                 # (_bin_pool reads it BIN_LAG backwards later)
                 seen = self._bin_seen(w)
-                seen[0].copy_(pool["ctl"][:1], non_blocking=True)
+                # pool_next and the sum passes' sticky fault word (GbCtl)
+                seen[0].copy_(pool["ctl"][:GB_CTL_READ], non_blocking=True)
                 seen[1].record(torch.cuda.current_stream(grid_grad.device))
                 fx_redo()
                 span = self._ev_open("fx_sum")
@@ -617,8 +626,8 @@ class FusedMLRenderer:
         """the next of BIN_LAG + 1 pinned (count, event) slots, in turn"""
         ring = getattr(w, "_bin_ring", None)
         if ring is None:
-            ring = w._bin_ring = [[torch.zeros(1, dtype=torch.int32, pin_memory=True), None,
-                                   -1] for _ in range(self.BIN_LAG + 1)]
+            ring = w._bin_ring = [[torch.zeros(GB_CTL_READ, dtype=torch.int32, pin_memory=True),
+                                   None, -1] for _ in range(self.BIN_LAG + 1)]
             w._bin_n = 0
         slot = ring[w._bin_n % len(ring)]
         slot[1] = torch.cuda.Event()
@@ -647,6 +656,12 @@ class FusedMLRenderer:
                 slot = ring[n % len(ring)]
                 if slot[2] == n and slot[1] is not None:
                     slot[1].synchronize()
+                    if int(slot[0][GB_SUM_FAULT]) != 0:
+                        raise RuntimeError(
+                            "binned grid scatter: a sum pass refused a page run (GbCtl "
+                            f"sum_fault {int(slot[0][GB_SUM_FAULT]):#x}) at or before the "
+                            f"backward {self.BIN_LAG} steps back; that step's grid gradient "
+                            "is incomplete (the page pool or its descriptors were corrupted)")
                     used = int(slot[0][0])
                     if used * 8 > need * 7:      # above 7/8: grow to 1.5x what was used
                         need = used * 3 // 2 + 64

@@ -308,3 +308,65 @@ def test_bin_pass_without_ctl_reset_stays_in_bounds(cuda):
     _canaries_intact(buf, lay, pool)
     assert int(buf["ctl"][1 + 15]) == 8                  # counted on ...
     assert int(buf["ctl"][17]) & 4                       # ... but refused
+
+
+def test_sum_pass_run_fault_is_sticky_and_raised(cuda):
+    """the sum pass skipped a page run past its page and set the
+    fault word, but the step's check had already run, so nothing read it.
+    Now the run is also recorded in GbCtl's sticky sum_fault word (not cleared
+    by the per-step reset), and the renderer raises when it reads it back."""
+    L = lib()
+    lay = L.bin_layout()
+    PAGE = lay["page"]
+    lv = LY.grid_levels(16.0)
+    hs = lv["hsize"]
+    rng = np.random.default_rng(3)
+    n = 2000
+    f = _field(rng.integers(-9, 9, n))[0]
+    pg = np.zeros(PAGE, np.int64)
+    pg[:n] = _pack(rng.integers(0, int(hs[12]), n), f, f, lay)
+    pool = 2
+    buf = _pool(cuda, lay, pool, [pg], [12 | (n << 8)])
+    st = torch.cuda.current_stream().cuda_stream
+    L.grid_bin(hs.ctypes.data, buf["ctl"].data_ptr(), buf["meta"].data_ptr(),
+               buf["pin"].data_ptr(), buf["pout"].data_ptr(), buf["desc"].data_ptr(),
+               buf["lpages"].data_ptr(), pool, 64, st)
+    torch.cuda.synchronize()
+    assert int(buf["ctl"][17]) == 0 and int(buf["ctl"][18]) == 0
+    # one slice's run pushed past the page end
+    desc = buf["desc"][:lay["bins"]]
+    b = int(torch.nonzero(desc >> 16).view(-1)[0])
+    buf["desc"][b] = (int(desc[b]) & 0xffff0000) | (PAGE - 3)
+    sc = torch.full((16,), 1.0, device=cuda)
+    redo = torch.zeros(1, device=cuda, dtype=torch.int32)
+    grad = torch.zeros(2 * int(lv["n_entries"]) + 64, device=cuda)
+    L.grid_sum(lv["offset"].ctypes.data, hs.ctypes.data, buf["ctl"].data_ptr(),
+               buf["desc"].data_ptr(), buf["lpages"].data_ptr(), buf["pout"].data_ptr(), pool,
+               sc.data_ptr(), redo.data_ptr(), grad.data_ptr(), 0, 16, st)
+    torch.cuda.synchronize()
+    _canaries_intact(buf, lay, pool)
+    assert int(buf["ctl"][17]) & 8 and int(buf["ctl"][18]) & 8
+    # the renderer: a sticky word read back raises at the next pool sizing
+    from radnerf_amd.fused import GB_SUM_FAULT
+    assert GB_SUM_FAULT == 18
+
+
+def test_renderer_raises_on_sum_fault(cuda):
+    """End to end at scale 16: the binned renderer reads GbCtl back with the
+    page count; a sticky sum_fault makes the pool sizing BIN_LAG backwards
+    later raise RuntimeError instead of stepping on a partial gradient.  A clean
+    run leaves the word 0."""
+    B, K, scale = 512, 2, 16.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    assert r.grid_bin
+    for _ in range(4):
+        _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    torch.cuda.synchronize()
+    assert int(r.ws._bin["ctl"][18]) == 0 and int(r.ws._bin["ctl"][17]) == 0
+    r.ws._bin["ctl"][18] = 8                        # as a refused run leaves it
+    with pytest.raises(RuntimeError, match="sum pass refused a page run"):
+        for _ in range(r.BIN_LAG + 2):
+            _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    r.ws._bin["ctl"][18] = 0
+    release_renderers()

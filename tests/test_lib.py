@@ -91,6 +91,97 @@ def test_missing_library_fails_loudly(tmp_path, monkeypatch):
         _lib._Lib(str(tmp_path / "librn.so"))
 
 
+def _fake_library(tmp_path, table, version=_lib.ABI_VERSION, name="librn_fake.so"):
+    """A stand-in library exporting only the load-time ABI entries (no kernel:
+    the checks must refuse it before any entry is bound)."""
+    src = tmp_path / "fake.c"
+    sig = "" if table is None else (
+        'const char* rn_abi_signatures(void) { return "%s"; }\n' % table)
+    src.write_text(f"int rn_version(void) {{ return {version}; }}\n"
+                   'const char* rn_last_error(void) { return ""; }\n'
+                   "void rn_set_debug_flags(int f) { (void)f; }\n" + sig)
+    out = tmp_path / name
+    subprocess.check_call(["gcc", "-shared", "-fPIC", str(src), "-o", str(out)])
+    return str(out)
+
+
+def test_library_signature_table_matches_binding():
+    """librn.so's rn_abi_signatures() (generated from the header at build time)
+    equals the binding's argument lists entry by entry, and the generator reads
+    the header the same way."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "rad-nerf_amd", "csrc"))
+    import gen_sig
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.rn_abi_signatures.restype = ctypes.c_char_p
+    have = _lib.parse_signature_table(lib.rn_abi_signatures().decode())
+    want = _lib.binding_signatures()
+    assert {n: have[n] for n in want} == want
+    assert _lib.parse_signature_table(gen_sig.table(open(HEADER).read())) == have
+    assert set(have) == set(_declared())
+
+
+def test_mismatched_signature_table_is_refused(tmp_path):
+    """a library built from another revision of the header
+    (one entry's arguments changed under the same RN_ABI_VERSION, as the A/B
+    leg that called rn_gate_bwd with shifted arguments) fails at load with an
+    ImportError naming the entry -- before any entry is bound or called."""
+    good = dict(_lib.binding_signatures())
+    bad = dict(good)
+    bad["rn_gate_bwd"] = good["rn_gate_bwd"] + "p"        # one more pointer argument
+    table = ";".join(f"{k}:{v}" for k, v in bad.items())
+    with pytest.raises(ImportError, match=r"another revision.*rn_gate_bwd: library "):
+        _lib._Lib(_fake_library(tmp_path, table))
+    # a missing entry is named too
+    del bad["rn_gate_bwd"]
+    table = ";".join(f"{k}:{v}" for k, v in bad.items())
+    with pytest.raises(ImportError, match="rn_gate_bwd: library missing"):
+        _lib._Lib(_fake_library(tmp_path, table, name="librn_fake2.so"))
+    # a library without the table (built before ABI 9), or of another ABI version
+    with pytest.raises(ImportError, match="no rn_abi_signatures"):
+        _lib._Lib(_fake_library(tmp_path, None, name="librn_fake3.so"))
+    with pytest.raises(ImportError, match="ABI 8, binding expects"):
+        _lib._Lib(_fake_library(tmp_path, None, version=8, name="librn_fake4.so"))
+    # the same table as the binding's passes the checks (then binding the
+    # entries fails: the stand-in exports none of them)
+    table = ";".join(f"{k}:{v}" for k, v in good.items())
+    with pytest.raises(AttributeError, match="rn_ray_aabb_intersect"):
+        _lib._Lib(_fake_library(tmp_path, table, name="librn_fake5.so"))
+
+
+def _doc_argtypes():
+    """every `L.rn_x.argtypes = ...` assignment of INTEGRATION.md's ctypes
+    binding, evaluated: {name: codes} (p pointer, i int32, l int64, ...)"""
+    text = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    env = dict(P=ctypes.c_void_p, I32=ctypes.c_int32, I64=ctypes.c_int64, F32=ctypes.c_float,
+               F64=ctypes.c_double, U64=ctypes.c_uint64, ctypes=ctypes)
+    code = {ctypes.c_void_p: "p", ctypes.c_int32: "i", ctypes.c_int64: "l",
+            ctypes.c_float: "f", ctypes.c_double: "d", ctypes.c_uint64: "u"}
+    out = {}
+    for m in re.finditer(r"L\.(rn_\w+)\.argtypes\s*=\s*", text):
+        expr, depth = "", 0
+        for line in text[m.end():].split("\n"):
+            line = line.split("#")[0]
+            expr += line.rstrip().rstrip("\\") + " "
+            depth += line.count("(") + line.count("[") - line.count(")") - line.count("]")
+            if depth == 0 and not line.rstrip().endswith("\\"):
+                break
+        out[m.group(1)] = "".join(code[t] for t in eval(expr, env))
+    return out
+
+
+def test_integration_doc_argtypes_match_library():
+    """INTEGRATION.md's ctypes binding (what a maintainer copies into the
+    reference) declares each entry exactly as the library was built (its
+    signature table) -- the round-6 check found two stale lines there."""
+    doc = _doc_argtypes()
+    assert len(doc) >= 15
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    lib.rn_abi_signatures.restype = ctypes.c_char_p
+    have = _lib.parse_signature_table(lib.rn_abi_signatures().decode())
+    assert {n: have.get(n) for n in doc} == doc
+
+
 def test_reference_dropin_module_names():
     """`import vren` from rad-nerf_amd/ exposes the reference binding's 12 names
     (binding.cpp:234-251)."""

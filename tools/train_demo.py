@@ -58,6 +58,7 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
     gen.manual_seed(1234)
     curve, redo_steps = [], 0
     acc_rgb, n_acc = 0.0, 0
+    tail, tail_n = 0.0, 0                # the last 200 steps' mean rgb loss
     torch.cuda.synchronize()
     t0 = time.time()
     for s in range(steps):
@@ -68,6 +69,9 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
             redo_steps += int(tr.renderer.ws._fx[3].item())
         acc_rgb += float(terms["rgb"])
         n_acc += 1
+        if s >= steps - 200:
+            tail += float(terms["rgb"])
+            tail_n += 1
         if (s + 1) % 50 == 0:
             mse = acc_rgb / n_acc
             curve.append({"step": s + 1, "rgb_mse": round(mse, 6),
@@ -79,7 +83,9 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
     return {"grid_fx": grid_fx, "binned": bool(grid_fx and tr.renderer.grid_bin),
             "seconds": round(time.time() - t0, 2), "curve": curve,
             "fx_redo_steps": redo_steps if grid_fx else None,
-            "final_psnr": curve[-1]["psnr"], "params": params}
+            "final_psnr": curve[-1]["psnr"],
+            "psnr_last200": round(-10 * math.log10(max(tail / max(tail_n, 1), 1e-12)), 3),
+            "params": params}
 
 
 def main():
