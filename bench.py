@@ -162,6 +162,9 @@ def parse():
     ap.add_argument("--grid-split", type=int, default=8, choices=range(16), metavar="[0-15]",
                     help="N>1, binned fold: the grid levels [this, 16) are summed first and "
                          "their all-reduce starts while levels [0, this) are summed")
+    ap.add_argument("--fx-f32-levels", default="",
+                    help="comma-separated hash levels whose grid gradient goes in by fp32 "
+                         "atomics instead of fixed point (e.g. 4,5,6,7,8; default none)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the world size, print the ranks seen and exit "
                          "(no GPU work; with --backend gloo it runs on CPU)")
@@ -313,6 +316,8 @@ def main():
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     if args.grid_fx is not None:
         r.grid_fx = bool(args.grid_fx)
+    if args.fx_f32_levels:
+        r.fx_f32_levels = tuple(int(x) for x in args.fx_f32_levels.split(","))
     if args.grid_bin is not None:
         r.grid_bin = bool(args.grid_bin) and r.grid_fx
     if args.level_fwd is not None:
@@ -772,6 +777,7 @@ def main():
                           "field_fwd": "levels" if getattr(r, "level_fwd", False) else "merged",
                           "grid_scatter": ("binned" if binned else "fixed-point atomics"
                                            if r.grid_fx and not args.split_bwd else "fp32 atomics"),
+                          "fx_f32_levels": list(getattr(r, "fx_f32_levels", ())),
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": (f"pinned{args.pinned_sim}-rank0-sim" if args.pinned_sim

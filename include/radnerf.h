@@ -271,11 +271,11 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * memory side serves them ~27 % faster than f32 adds), so those levels'
  * gradients are order-independent and bitwise reproducible.
  * rn_grid_fx_fold then (1) sets *fx_redo when a level's largest record reached
- * 2^28 units or was not finite, or when the level's entry sum differs from its
+ * 2^30 units or was not finite, or when the level's entry sum differs from its
  * record sum, plain or weighted (an int32 entry wrapped: many same-sign
  * records; two opposite wraps cancel only in the plain sum), writes the
  * next step's scales
- * (2^(23 - e), |record| < 2^e, capped so the largest entry stays < 2^28 units;
+ * (2^(27 - e), |record| < 2^e, capped so the largest entry stays < 2^29 units;
  * a dense level's first fixed-point step 2^(14 - e)) to fx_scale_next and clears
  * the statistics, (2) adds fx_acc * 2^-e_l into grid_grad (skipped when *fx_redo)
  * and re-zeroes fx_acc.  The caller then launches rn_field_bwd_merged with

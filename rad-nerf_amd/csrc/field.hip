@@ -362,16 +362,18 @@ __device__ __forceinline__ void ig_check(int32_t old, int32_t lo, int32_t hi, ui
 // against 20.9 for f32 (profiles/r01/atomic_probe.json), and the sums are
 // exact, so these levels' gradients are bitwise reproducible.  e_l comes from
 // the previous step's largest record of the level (rn_grid_fx_fold): that
-// record maps to < 2^23 units, leaving 2^8 max-size records of headroom per
-// entry (an entry of a hashed level takes ~77 records per C3 step, of mixed
-// sign).  The kernel records this step's largest |record| per level; when it
-// exceeds 2^28 units (32x growth) or is not finite, rn_grid_fx_fold discards
-// the fixed-point sums and the GM 3 launch redoes the grid scatter in fp32.
+// record maps to < 2^27 units (2^23 until round 6; FX_TARGET_BITS below),
+// leaving 2^4 max-size records of headroom per entry (an entry of a hashed
+// level takes ~77 records per C3 step, of mixed sign, and its largest sum
+// stays within 2^1.2 of the largest record).  The kernel records this step's
+// largest |record| per level; when it reaches 2^30 units (8x growth) or is not
+// finite, rn_grid_fx_fold discards the fixed-point sums and the GM 3 launch
+// redoes the grid scatter in fp32.
 // The first step of a workspace (scale 0) uses fp32 atomics and measures the
 // records; the dense levels (few requests, but entries that sum hundreds of
 // records) go fixed point from then on with a scale capped by their largest
 // entry (k_fx_check).
-// An int32 entry can still wrap with every record under 2^28 units (many
+// An int32 entry can still wrap with every record under 2^30 units (many
 // same-sign records on one entry); the kernel therefore also sums each
 // level's integer records exactly (int64), and rn_grid_fx_fold sums the
 // level's int32 entries exactly: a wrapped entry makes the two differ by a
@@ -1909,31 +1911,39 @@ k_fx_esum(GridMeta gm, const float* __restrict__ scale, const int32_t* __restric
 // Fixed-point step bookkeeping (one wave): redo flag of this step, the next
 // step's per-level scales from this step's largest records, statistics reset.
 // Scale 2^(FX_TARGET_BITS - e) with |record| < 2^e: the largest record maps
-// to < 2^23 units.  A level whose largest record reached 2^28 units under the
-// current scale (32x growth since the step the scale came from), or a
+// to < 2^27 units.  A level whose largest record reached 2^30 units under the
+// current scale (8x growth since the step the scale came from), or a
 // non-finite one, or whose entries wrapped (entry sum != record sum), sets the
 // redo flag: rn_grid_fx_fold then discards the fixed-point sums and the GM 3
 // launch recomputes the grid gradient in fp32.
 // Headroom measured on C3 over 12 Adam steps (tools/fx_diag.py): the largest
 // |entry| of a hashed level stays within 2^1.2 of its largest record, so at
-// 2^23 units it sits ~2^7 below the int32 range; the unit 2^-23 of the level's
-// largest record leaves 0.01 % of the non-zero fp32 entries at 0 (2^19:
-// 0.15 %).  A dense (coarse) level's entry sums up to hundreds of records, so
-// its scale is also capped by this step's largest |entry|: it maps to < 2^28
-// units (2^3 of headroom for growth; the first step's entries are read from
-// the fp32 grid_grad); a dense level with no entry measured maps its largest
-// record to < 2^14 units.
+// 2^27 units it sits ~2^3 below the int32 range.  A dense (coarse) level's
+// entry sums up to hundreds of records, so its scale is also capped by this
+// step's largest |entry|: it maps to < 2^29 units (2^2 of headroom for growth;
+// the first step's entries are read from the fp32 grid_grad); a dense level
+// with no entry measured maps its largest record to < 2^14 units.
+// Why these units (round 6; tools/fx_units_probe.py,
+// profiles/r06/fxunits/): FusedAdam's eps 1e-15 turns any non-zero gradient
+// into an lr-sized step, so an entry below half a unit (flushed to 0) moves
+// the update as much as a wrong sign.  C3, 3 Adam steps, largest per-level
+// update difference from fp32 (fp32 with the rays reversed: <= 0.07 %):
+// 2048 rays 2.66 % at (23, 28, 28) -> 1.14 % at (27, 29, 30); 8192 rays 1.02
+// -> 0.38 %; flushed entries 0.031 -> 0.005 %; no step redone in 1,150
+// probe and training steps; 1000 training steps end within 0.03 dB of fp32
+// either way.  (26, 30, 30) redid one of 1000 training steps (entry cap too
+// close to 2^31).
 #ifndef FX_TARGET_BITS              // (-D overrides: unit studies, tools/fx_units_probe.py)
-#define FX_TARGET_BITS 23
+#define FX_TARGET_BITS 27
 #endif
 #ifndef FX_ENTRY_BITS
-#define FX_ENTRY_BITS 28
+#define FX_ENTRY_BITS 29
 #endif
 #define FX_DENSE_FIRST_BITS 14
 #ifndef FX_GROWTH_BITS
-#define FX_GROWTH_BITS 28
+#define FX_GROWTH_BITS 30
 #endif
-#define FX_GROWTH_UNITS ((float)(1u << FX_GROWTH_BITS))   // 2^28
+#define FX_GROWTH_UNITS ((float)(1u << FX_GROWTH_BITS))   // 2^30
 // Binned mode (ctl != NULL, rn_grid_binned_fold): records are e5m17 (rn_bin.h),
 // summed exactly in int64, so there is no entry cap and no wrap check; the
 // largest record maps to < 2^GB_TARGET_BITS = 2^38 units (256x headroom below
@@ -1977,7 +1987,7 @@ k_fx_check(uint32_t hashed_mask, const float* __restrict__ scale_cur,
             int bits = (binned ? GB_TARGET_BITS : FX_TARGET_BITS) - e;
             if (binned) {
                 // int64 sums: no entry cap
-            } else if (em != 0u) {                       // the largest entry stays < 2^28 units
+            } else if (em != 0u) {                       // the largest entry stays < 2^29 units
                 int ee;
                 frexpf(__uint_as_float(em), &ee);
                 bits = min(bits, FX_ENTRY_BITS - ee);

@@ -17,7 +17,9 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#ifndef GB_PAGE                   // (-D override: page-size studies)
 #define GB_PAGE 8192              // records per page (64 KB)
+#endif
 #define GB_SLICE_BITS 12          // largest slice: 4096 entries (64 KB of int64 pairs in LDS)
 #define GB_SLICE (1u << GB_SLICE_BITS)
 #define GB_MIN_SLICE_BITS 6       // smallest slice: 64 entries

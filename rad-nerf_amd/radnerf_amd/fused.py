@@ -288,6 +288,14 @@ class FusedMLRenderer:
         # 63.5 records x 95 samples; tools/records_sim.py), x 1.15
         self.bin_records_per_pair = 6912
         self.min_chunk = 512
+        # hash levels whose grid gradient goes in by fp32 atomics instead of
+        # fixed point (int32 or binned): () = none, every level an exact
+        # integer sum (bitwise reproducible).  (3, ..., 8) at C3 brings the
+        # per-entry 3-step Adam difference from fp32 from 1.1 % to 0.3 %
+        # (levels 3-8 hold most of the int32 form's flushed entries) at the
+        # cost of those levels' reproducibility (bench.py
+        # --fx-f32-levels)
+        self.fx_f32_levels = ()
         # optional short first chunk per block (starts the scatter sooner):
         # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms); round 5
         # again: C3 1185-1187 and C5 732-736 at 0-512 (profiles/r05/chunk5/)
@@ -354,6 +362,14 @@ class FusedMLRenderer:
         if getattr(self, "_side_stream", None) is None:
             self._side_stream = torch.cuda.Stream(dev)
         return self._side_stream
+
+    def _f32_level_index(self, dev):
+        key = (tuple(sorted(int(l) for l in self.fx_f32_levels)), str(dev))
+        if getattr(self, "_f32_idx", (None,))[0] != key:
+            if any(not 0 <= l < 16 for l in key[0]):
+                raise ValueError(f"fx_f32_levels: hash levels are 0..15, got {key[0]}")
+            self._f32_idx = (key, torch.tensor(key[0], dtype=torch.int64, device=dev))
+        return self._f32_idx[1]
 
     def kernel_times_ms(self):
         """{kernel: [ms per launch]} of the traced launches (synchronises)."""
@@ -513,6 +529,10 @@ class FusedMLRenderer:
             if use_fx:
                 acc, scales, stats, redo = w.fx_buffers(grid_grad.numel(), grid_grad.device)
                 cur, nxt = scales[w.fx_i], scales[1 - w.fx_i]
+                if self.fx_f32_levels:
+                    # these levels go in by fp32 atomics this step (a zero
+                    # scale selects the kernel's per-level fp32 path)
+                    cur.index_fill_(0, self._f32_level_index(cur.device), 0.0)
                 fx = (acc.data_ptr(), cur.data_ptr(), stats.data_ptr(), None, 2)
             if use_bin:
                 pool = self._bin_pool(w)

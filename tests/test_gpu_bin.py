@@ -20,7 +20,7 @@ import torch
 
 from radnerf_amd import layout as LY
 from radnerf_amd._lib import lib
-from radnerf_amd.fused import get_renderer, ml_render_fused
+from radnerf_amd.fused import get_renderer, ml_render_fused, release_renderers
 from test_gpu_ml import FX_LEVEL_TOL, _run, _setup, check_fx_vs_fp32
 
 pytestmark = pytest.mark.gpu
@@ -356,7 +356,7 @@ def test_renderer_raises_on_sum_fault(cuda):
     page count; a sticky sum_fault makes the pool sizing BIN_LAG backwards
     later raise RuntimeError instead of stepping on a partial gradient.  A clean
     run leaves the word 0."""
-    B, K, scale = 512, 2, 16.0
+    B, K, scale = 1024, 2, 16.0               # (rays x sub-NeRFs > 1024: fixed point)
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
     assert r.grid_bin

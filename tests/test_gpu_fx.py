@@ -143,11 +143,15 @@ def test_fx_entry_wrap_sets_redo(cuda):
 # (B, K, scale): C3's shape (int32 fixed point, atomics), C4's branch (K = 4,
 # scale 16, exponential steps) and a C5-shaped one (K = 8, scale 16), both on
 # the binned scatter (the default at scale 16)
-PER_ENTRY_SHAPES = [(2048, 2, 0.5), (4096, 4, 16.0), (2048, 8, 16.0)]
+# (B, K, scale, fp32 levels, bar on the 3-step Adam difference per level):
+# the int32 form at C3 measured 1.14 % with round 6's units (2.66 % before),
+# 0.3 % with levels 3-8 on fp32 atomics (fx_f32_levels); e5m17 0.25 %
+PER_ENTRY_SHAPES = [(2048, 2, 0.5, (), 0.02), (2048, 2, 0.5, (3, 4, 5, 6, 7, 8), 0.005),
+                    (4096, 4, 16.0, (), 0.01), (2048, 8, 16.0, (), 0.01)]
 
 
-@pytest.mark.parametrize("B,K,scale", PER_ENTRY_SHAPES)
-def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
+@pytest.mark.parametrize("B,K,scale,f32_levels,bar", PER_ENTRY_SHAPES)
+def test_fx_per_entry_agreement(cuda, capsys, B, K, scale, f32_levels, bar):
     """fixed point per ENTRY, not only per-level norms.  One
     step fixed point vs fp32 over every level: the share of entries non-zero
     in fp32 but zero in fixed point, and the sign agreement of the entries
@@ -161,6 +165,7 @@ def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
     assert r.grid_fx and r.grid_bin == (scale > 0.5)
+    r.fx_f32_levels = f32_levels
     lv = LY.grid_levels(scale)
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)              # scales
     unit = (1.0 / r.ws._fx[1][r.ws.fx_i].clamp_min(1e-30)).cpu()
@@ -207,7 +212,8 @@ def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
     rels, floor = upd("fx", "fp32"), upd("fp32_reordered", "fp32")
     rel = max(rels)
     with capsys.disabled():
-        print(f"\nfx per entry B{B} K{K} s{scale} ({'binned' if r.grid_bin else 'int32'}): "
+        print(f"\nfx per entry B{B} K{K} s{scale} ({'binned' if r.grid_bin else 'int32'}"
+              f"{', fp32 levels ' + str(f32_levels) if f32_levels else ''}): "
               f"{f_lost:.4%} of the non-zero fp32 entries are 0 in fixed point; "
               f"sign agreement above one unit {f_agree:.5%} ({n_big} entries); "
               f"3 Adam steps: per-level update difference max {rel:.3e} "
@@ -215,9 +221,10 @@ def test_fx_per_entry_agreement(cuda, capsys, B, K, scale):
               f"{max(floor):.3e}")
         print("  per level fx-fp32 " + " ".join(f"{x:.3f}" for x in rels))
         print("  per level fp32-fp32 reordered " + " ".join(f"{x:.3f}" for x in floor))
+    r.fx_f32_levels = ()
     assert f_agree >= 0.999
     assert f_lost <= 0.05
-    assert rel <= 0.04
+    assert rel <= bar
 
 
 def _fx_weight(i):

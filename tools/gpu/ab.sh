@@ -3,6 +3,10 @@
 # tests on the new build, then the headline bench and the C5 per-GPU shape
 # alternating old / new (RADNERF_LIB), so both see the same card and clocks.
 # usage: tools/gpu/ab.sh <tag> [old_lib]   (VARIANTS="old new b": librn_<v>.so, new = librn.so)
+# Every leg runs HEAD's Python binding: a library built from another revision
+# of include/radnerf.h is refused at load (ABI 9 signature table), so an old
+# leg must be built from a tree with the same C ABI (round 5's failed leg,
+# DESIGN §5, called rn_gate_bwd with shifted arguments).
 set -u
 mkdir -p gpurun_out
 TAG=${1:-ab}

@@ -54,6 +54,9 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
     g = Ray_Gate(K, seed=4).to(dev)
     tr = Trainer(m, g, B, lr=1e-2, lambda_cv_importance=1e-2)
     tr.renderer.grid_fx = grid_fx
+    # $FX_F32_LEVELS="4,5,6,7,8": those levels by fp32 atomics (fused.fx_f32_levels)
+    tr.renderer.fx_f32_levels = tuple(int(x) for x in os.environ.get("FX_F32_LEVELS", "").split(",")
+                                      if x)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234)
     curve, redo_steps = [], 0
