@@ -300,7 +300,10 @@ int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
  * GbCtl block (u32 pages taken, u32 pages per level [16], u32 fault bits:
  * 1 a page meta with a level >= 16 or more than 8192 records, 2 a record
  * index outside its level, 4 a level list past the pool, 8 a page id or run
- * outside the pool / page -- refused, never followed), zero before pass 1;
+ * outside the pool / page -- refused, never followed; then u32 sum_fault:
+ * the sum passes' bit 8, sticky -- rn_field_bwd_merged zeroes only the first
+ * 72 B each step, so a caller reads it back to learn that a sum pass, which
+ * runs after the step's redo decision, skipped a run), zero before pass 1;
  * page_meta [pool_pages] u32 (level | count << 8); pages_in / pages_out
  * [pool_pages][8192] u64; desc
  * [pool_pages][256] u32; level_pages [16][pool_pages] u32.
