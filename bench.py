@@ -165,6 +165,9 @@ def parse():
     ap.add_argument("--fx-f32-levels", default="",
                     help="comma-separated hash levels whose grid gradient goes in by fp32 "
                          "atomics instead of fixed point (e.g. 4,5,6,7,8; default none)")
+    ap.add_argument("--bin-f32-levels", type=int, default=None, choices=range(17), metavar="[0-16]",
+                    help="binned scatter: the coarse levels [0, n) by fp32 atomics instead of page "
+                         "records (default: the renderer's choice by shape)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, check the world size, print the ranks seen and exit "
                          "(no GPU work; with --backend gloo it runs on CPU)")
@@ -316,6 +319,8 @@ def main():
     r.merged_bwd = r.merged_bwd and not args.split_bwd
     if args.grid_fx is not None:
         r.grid_fx = bool(args.grid_fx)
+    if args.bin_f32_levels is not None:
+        r.bin_f32_levels = args.bin_f32_levels
     if args.fx_f32_levels:
         r.fx_f32_levels = tuple(int(x) for x in args.fx_f32_levels.split(","))
     if args.grid_bin is not None:
@@ -778,6 +783,7 @@ def main():
                           "grid_scatter": ("binned" if binned else "fixed-point atomics"
                                            if r.grid_fx and not args.split_bwd else "fp32 atomics"),
                           "fx_f32_levels": list(getattr(r, "fx_f32_levels", ())),
+                          "bin_f32_levels": int(getattr(r, "bin_f32_levels", 0)) if binned else None,
                           "samples_per_step_per_gpu": round(samples_per_step_rank),
                           "global_batch": B if args.pinned else B * world,
                           "parallelism": (f"pinned{args.pinned_sim}-rank0-sim" if args.pinned_sim

@@ -278,6 +278,18 @@ class FusedMLRenderer:
         # of memory-side atomics, which were 45 % of C5's field_bwd
         # (DESIGN §4 "Binned scatter")
         self.grid_bin = self.grid_fx and float(model.scale) > 0.5
+        # binned mode: the coarse levels [0, n) go in by fp32 atomics instead
+        # of page records.  A coarse record shares its 64-B request with its
+        # neighbours (dense levels, the first hashed ones) and the walk hides
+        # those atomics, while a page record costs 24 B of bin + sum traffic
+        # (round 6, tools/level_bin_probe.py, profiles/r06/level_bin/): all
+        # binned -> levels [0, n) fp32: C5 738 -> 763 M samples/s per GPU at
+        # n = 9, C4 599 -> 640 at n = 8 (beyond, the atomics bind).  Those
+        # levels' sums are then fp32 in arrival order (the fine levels' stay
+        # exact int64); exact int64 sums with u64 atomics were measured too
+        # and lost to fp32 (16-B entries double the requests of an x-pair;
+        # DESIGN §4)
+        self.bin_f32_levels = (9 if model.size >= 8 else 8) if self.grid_bin else 0
         # the int32 form's wrap checksums weight gradient element i by 4 i
         # (field.hip fx_weight), injective up to 2^28 elements: a larger table
         # (none of the reference's configs: 16 levels x 2^19 entries x 2
@@ -533,6 +545,9 @@ class FusedMLRenderer:
                     # these levels go in by fp32 atomics this step (a zero
                     # scale selects the kernel's per-level fp32 path)
                     cur.index_fill_(0, self._f32_level_index(cur.device), 0.0)
+                n32 = max(0, min(16, int(self.bin_f32_levels))) if use_bin else 0
+                if n32:
+                    cur[:n32].zero_()           # binned mode: coarse levels by fp32 atomics
                 fx = (acc.data_ptr(), cur.data_ptr(), stats.data_ptr(), None, 2)
             if use_bin:
                 pool = self._bin_pool(w)

@@ -129,7 +129,7 @@ def test_binned_matches_fp32_and_is_reproducible(cuda, B, K, scale):
     r = get_renderer(m, g, B)
     assert r.grid_fx
     assert r.grid_bin == (scale > 0.5)
-    r.grid_bin = True
+    r.grid_bin, r.bin_f32_levels = True, 0          # every level binned
     _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)      # fp32: scales
     _, gb1 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     assert check_fx_vs_fp32(m, gb1, g32, r, f"binned B{B} K{K} s{scale}") == 16
@@ -370,3 +370,28 @@ def test_renderer_raises_on_sum_fault(cuda):
             _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
     r.ws._bin["ctl"][18] = 0
     release_renderers()
+
+
+@pytest.mark.parametrize("B,K", [(1024, 4), (1024, 8)])
+def test_binned_default_coarse_levels_fp32(cuda, B, K):
+    """Round 6 default at scale 16: the coarse levels [0, n) go in by fp32
+    atomics (no page records), the rest binned.  Every level matches the fp32
+    gradient of the same step (FX_LEVEL_TOL), the binned levels are bitwise
+    identical step to step, the coarse levels took no pages."""
+    scale = 16.0
+    m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
+    r = get_renderer(m, g, B)
+    n = r.bin_f32_levels
+    assert r.grid_bin and n == (9 if K >= 8 else 8)
+    _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    _, gb1 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    assert check_fx_vs_fp32(m, gb1, g32, r, f"binned, levels [0, {n}) fp32, B{B} K{K}") == 16 - n
+    npg = r.ws._bin["ctl"][1:17].cpu()
+    assert int(npg[:n].sum()) == 0 and bool((npg[n:] > 0).all()), npg
+    _, gb2 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
+    lv = LY.grid_levels(scale)
+    for l, (a, b) in enumerate(zip(_levels(gb1[0], lv), _levels(gb2[0], lv))):
+        if l >= n:
+            assert torch.equal(a, b), l                  # exact integer sums
+        else:                                            # fp32 in arrival order
+            assert float((a - b).norm() / b.norm().clamp_min(1e-30)) <= 1e-5, l

@@ -38,6 +38,7 @@ def test_fx_matches_fp32_and_is_reproducible(cuda, B, K, scale):
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
     assert r.grid_fx
+    r.bin_f32_levels = 0          # (scale 16: every level fixed point, binned)
     _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     _, gfx1 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     n_fx = check_fx_vs_fp32(m, gfx1, g32, r, f"B{B} K{K} s{scale}")
@@ -168,7 +169,7 @@ def test_fx_per_entry_agreement(cuda, capsys, B, K, scale, f32_levels, bar):
     r.fx_f32_levels = f32_levels
     lv = LY.grid_levels(scale)
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)              # scales
-    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].clamp_min(1e-30)).cpu()
+    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].abs().clamp_min(1e-30)).cpu()
     _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     assert int(r.ws._fx[3][0]) == 0                                         # no redo
     r.grid_fx = False

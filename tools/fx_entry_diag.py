@@ -30,7 +30,7 @@ def main():
     r = get_renderer(m, g, B)
     lv = LY.grid_levels(scale)
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
-    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].clamp_min(1e-30)).cpu().numpy()
+    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].abs().clamp_min(1e-30)).cpu().numpy()
     _, gfx = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
     r.grid_fx = False
     _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)

@@ -75,7 +75,7 @@ def main():
     noise, seeds = S.noise(K, B), S.loss_seeds(B, K)
     run(o, d, noise, seeds)                      # the first (fp32) step measures the records
     run(o, d, noise, seeds)
-    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].clamp_min(1e-30)).cpu()
+    unit = (1.0 / r.ws._fx[1][r.ws.fx_i].abs().clamp_min(1e-30)).cpu()
     gfx = run(o, d, noise, seeds)
     redo_first = int(r.ws._fx[3][0])
     r.grid_fx = False

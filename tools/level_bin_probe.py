@@ -11,6 +11,9 @@ fold's ms (int32: k_fx_fold span; binned: bin + check + sum) and, from the
 all-binned run, each level's records per sample (the page fills).
 
     python tools/level_bin_probe.py [Lb ...]      (default 0 6 8 10 12 14)
+    python tools/level_bin_probe.py atomic bin0 bin8 ...   (explicit variants)
+(the renderer's own default of fp32 coarse levels, bin_f32_levels, is switched
+off: every variant sets its cut here)
 """
 import json
 import os
@@ -28,7 +31,11 @@ from radnerf_amd.networks import MNGP, Ray_Gate  # noqa: E402
 
 
 def main():
-    cuts = [int(x) for x in sys.argv[1:]] or [0, 6, 8, 10, 12, 14]
+    toks = sys.argv[1:] or ["0", "6", "8", "10", "12", "14"]
+    if all(t.isdigit() for t in toks):
+        variants = ["atomic"] + [f"bin{t}" for t in toks]
+    else:
+        variants = toks
     dev = torch.device("cuda")
     B = int(os.environ.get("STEP_B", 8192))
     K = int(os.environ.get("STEP_K", 2))
@@ -65,11 +72,10 @@ def main():
         n_samples.append(r.ws.meta[1].clone())
         r.backward(o, d, d, gt, bg, *sd, None, 1e-4, gg, mg, ag)
 
-    variants = ["atomic"] + [f"bin{c}" for c in cuts]
-
     def select(v):
         r.grid_bin = v != "atomic"
-        state["cut"] = None if v == "atomic" else int(v[3:])
+        r.bin_f32_levels = 0
+        state["cut"] = int(v[3:]) if v.startswith("bin") else None
 
     times = {v: [] for v in variants}
     kern = {v: {"field_bwd": [], "fold": []} for v in variants}
