@@ -426,16 +426,22 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
     const int lane = rn_lane();
     const uint32_t h = __builtin_amdgcn_readlane(W.head, 4 * s);
     constexpr bool odd = ODD;
+    // binned (GM 4); GM 5: binned with the even streams' levels (0-7) by fp32
+    // atomics, known at compile time -- that instantiation carries no page or
+    // record-encoding code (round 6: the renderer's default at scale 16 sends
+    // levels [0, 8-9) by fp32 atomics, FusedMLRenderer.bin_f32_levels)
+    constexpr bool BIN = GM == 4 || GM == 5;
+    constexpr bool F32S = GM == 5 && !ODD;
     // the level's scale as float bits selected on the scalar unit (gfx9 has
     // no scalar float compare: a float test here became a VALU compare + vcc
     // branch per issue)
     const uint32_t scb = GM >= 2 ? (uint32_t)__builtin_amdgcn_readfirstlane(
                                        (int)(odd ? __float_as_uint(W.fxB) : __float_as_uint(W.fxA)))
                                  : 0u;
-    const bool fx_lvl = (scb << 1) != 0u;       // 2^e_l > 0: fixed point; +-0: fp32 atomics
+    const bool fx_lvl = !F32S && (scb << 1) != 0u;   // 2^e_l > 0: fixed point; +-0: fp32 atomics
     const float sc_s = __uint_as_float(scb);
     asm volatile("" ::: "memory");
-    if (GM == 4 && fx_lvl) {
+    if (BIN && fx_lvl) {
         // the level's open page cannot take cnt more records: close it (its
         // level and fill, for the bin pass) and take the pool's next page
         const uint32_t n = odd ? W.nB : W.nA;
@@ -465,7 +471,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         const uint32_t w0 = base[rec];
         // byte offset of the lane's feature (GM 4: only the fp32 fallback
         // and the timing branches use it; the page record takes w0)
-        const uint32_t off = (GM == 4 ? 8u * ((odd ? W.loffB : W.loffA) + w0) : w0) + 4u * (lane & 1);
+        const uint32_t off = (BIN ? 8u * ((odd ? W.loffB : W.loffA) + w0) : w0) + 4u * (lane & 1);
         const uint32_t v = base[(1 + (lane & 1)) * W2_RING + rec];
         if (rn_dbg(dbg) & 1) {
             asm volatile("" :: "v"(off), "v"(v));
@@ -474,7 +480,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         } else if (rn_dbg(dbg) & 64) {      // ablation: non-returning i32 adds (timing only)
             (void)__builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(
                 (int)(__uint_as_float(v) * 1048576.0f), grad_rs, (int)off, 0, 0);
-        } else if (GM == 4 && fx_lvl) {
+        } else if (BIN && fx_lvl) {
             // binned: the 32 records go to the level's open page as 32 u64
             // (entry index, q0, q1), one 256-B store: lane 2r writes record
             // r's low word, lane 2r + 1 its high word
@@ -528,7 +534,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             W.offB = off;
             W.oldB = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(lo, G.lo, (int)off, 0, 0);
         } else {
-            if (GM == 2 || GM == 4) {                    // fp32 level: still tracked
+            if (GM == 2 || BIN) {                        // fp32 level: still tracked
                 const uint32_t ab = v & 0x7fffffffu;
                 if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             }
@@ -537,7 +543,7 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
         }
     }
     asm volatile("" ::: "memory");
-    if (GM == 4 && fx_lvl) {
+    if (BIN && fx_lvl) {
         if (odd) W.nB += cnt; else W.nA += cnt;
     }
     if (!DEFER) {           // (DEFER: the threshold drain advances every issued ring at once)
@@ -623,10 +629,10 @@ __device__ __forceinline__ void walk2_push(Walk2& W, bool e0, bool e1, uint32_t 
     // ring; it is overwritten before it is ever read)
     const uint32_t r0 = w2_wrap(W.tail + (e0 ? below : pushed));
     const uint32_t r1 = w2_wrap(W.tail + (e1 ? below + (e0 ? 1u : 0u) : pushed));
-    base[r0] = GM == 4 ? W.cur0 : 8u * (lvl_off + W.cur0);
+    base[r0] = GM >= 4 ? W.cur0 : 8u * (lvl_off + W.cur0);
     base[W2_RING + r0] = __float_as_uint(W.a00);
     base[2 * W2_RING + r0] = __float_as_uint(W.a01);
-    base[r1] = GM == 4 ? W.cur1 : 8u * (lvl_off + W.cur1);
+    base[r1] = GM >= 4 ? W.cur1 : 8u * (lvl_off + W.cur1);
     base[W2_RING + r1] = __float_as_uint(W.a10);
     base[2 * W2_RING + r1] = __float_as_uint(W.a11);
     W.tail = w2_wrap(W.tail + pushed);
@@ -1491,11 +1497,11 @@ k_field_bwd_merged(FieldArgs a, MergeArgs m, IntGrad G, FxGrad F) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) atomicAdd(g_rn_cyc + q, (unsigned long long)cyc[q]);
     }
-    if (GM == 4 && rn_lane() == 0) {             // close this wave's open pages
+    if (GM >= 4 && rn_lane() == 0) {             // close this wave's open pages
         if (pgA < G.pool_pages) G.page_meta[pgA] = (uint32_t)lvA | (nA << 8);
         if (pgB < G.pool_pages) G.page_meta[pgB] = (uint32_t)(RN_L - 1 - lvA) | (nB << 8);
     }
-    if (GM == 2 || GM == 4) {                    // this step's largest |record| per level
+    if (GM == 2 || GM >= 4) {                    // this step's largest |record| per level
         vmA = rn_wave_max_u32(vmA);
         vmB = rn_wave_max_u32(vmB);
         int64_t dA = sqA, dB = sqB;
@@ -2654,14 +2660,15 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
                         uint32_t* gb_page_meta, uint64_t* gb_pages, int32_t gb_pool_pages,
                         void* stream) {
     RN_CHECK_ARG(!igrad_lo || (igrad_carry && igrad_scale), "integer mode needs carry and scale");
-    RN_CHECK_ARG(fx_mode == 0 || fx_mode == 2 || fx_mode == 3 || fx_mode == 4,
-                 "fx_mode: 0, 2, 3 or 4");
+    RN_CHECK_ARG(fx_mode == 0 || fx_mode == 2 || fx_mode == 3 || fx_mode == 4 || fx_mode == 5,
+                 "fx_mode: 0, 2, 3, 4 or 5");
+    const bool binned = fx_mode == 4 || fx_mode == 5;
     RN_CHECK_ARG(fx_mode != 2 || (fx_acc && fx_scale && fx_stats && feat_cache),
                  "fixed-point mode needs acc, scale, stats and the encoding cache");
-    RN_CHECK_ARG(fx_mode != 4 || (fx_scale && fx_stats && feat_cache && gb_ctl && gb_page_meta &&
+    RN_CHECK_ARG(!binned || (fx_scale && fx_stats && feat_cache && gb_ctl && gb_page_meta &&
                                   gb_pages && gb_pool_pages >= 1),
                  "binned mode needs scale, stats, the encoding cache and the page pool");
-    for (int l = 0; fx_mode == 4 && l < RN_L; ++l)
+    for (int l = 0; binned && l < RN_L; ++l)
         RN_CHECK_ARG(level_hsize[l] <= (1u << GB_IDX_BITS) &&
                      level_hsize[l] <= ((uint32_t)GB_MAX_BINS << GB_SLICE_BITS),
                      "binned mode: a level has more than 2^20 entries");
@@ -2705,7 +2712,7 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
         G.bytes = 2 * a.grid_bytes;            // int32 arrays, same size as the f32 grad
         G.lo_ptr = igrad_lo; G.carry_ptr = igrad_carry; G.scale_ptr = igrad_scale;
     }
-    if (fx_mode == 4) {
+    if (binned) {
         if (hipMemsetAsync(gb_ctl, 0, GB_CTL_RESET_BYTES, st) != hipSuccess) {
             rn_set_error("%s: page pool reset failed", __func__);
             return 2;
@@ -2722,8 +2729,9 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
     }
     const dim3 blk(BWD_WAVES * 64);
     if constexpr (RN_ABL) {                     // timing studies (librn_abl.so only)
-        if (a.dbg && (fx_mode == 4 || fx_mode == 2 || (fx_mode == 0 && !igrad_lo))) {
-            if (fx_mode == 4) k_field_bwd_merged<CACHE_READ, true, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
+        if (a.dbg && (binned || fx_mode == 2 || (fx_mode == 0 && !igrad_lo))) {
+            if (fx_mode == 5) k_field_bwd_merged<CACHE_READ, true, 5><<<blocks, blk, 0, st>>>(a, m, G, F);
+            else if (fx_mode == 4) k_field_bwd_merged<CACHE_READ, true, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
             else if (fx_mode == 2) k_field_bwd_merged<CACHE_READ, true, 2><<<blocks, blk, 0, st>>>(a, m, G, F);
             else if (feat_cache) k_field_bwd_merged<CACHE_READ, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
             else k_field_bwd_merged<CACHE_NONE, true, 0><<<blocks, blk, 0, st>>>(a, m, G, F);
@@ -2731,7 +2739,9 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
             return 0;
         }
     }
-    if (fx_mode == 4) {
+    if (fx_mode == 5) {
+        k_field_bwd_merged<CACHE_READ, false, 5><<<blocks, blk, 0, st>>>(a, m, G, F);
+    } else if (fx_mode == 4) {
         k_field_bwd_merged<CACHE_READ, false, 4><<<blocks, blk, 0, st>>>(a, m, G, F);
     } else if (fx_mode == 2) {
         k_field_bwd_merged<CACHE_READ, false, 2><<<blocks, blk, 0, st>>>(a, m, G, F);

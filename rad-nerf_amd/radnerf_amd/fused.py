@@ -551,7 +551,9 @@ class FusedMLRenderer:
                 fx = (acc.data_ptr(), cur.data_ptr(), stats.data_ptr(), None, 2)
             if use_bin:
                 pool = self._bin_pool(w)
-                fx = (None, cur.data_ptr(), stats.data_ptr(), None, 4)
+                # fx_mode 5: levels 0-7 (the walk's even streams) are fp32 by
+                # construction, so that walk carries no page code for them
+                fx = (None, cur.data_ptr(), stats.data_ptr(), None, 5 if n32 >= 8 else 4)
                 gb = (pool["ctl"].data_ptr(), pool["meta"].data_ptr(), pool["recs"].data_ptr(),
                       pool["pages"])
             if self.int_grad:
