@@ -286,7 +286,11 @@ int rn_field_bwd_merged(const float* ts, const int32_t* ray_of, const float* ray
  * fx_mode 4: binned (rn_grid_bin below): the fixed-point records (e5m17, the
  * largest < 2^38 units) are appended to the gb_* page pool (gb_ctl is reset
  * by the call) instead of atomically added; rn_grid_binned_fold then bins
- * and sums them into grid_grad (fx_acc unused).                            */
+ * and sums them into grid_grad (fx_acc unused).  A level whose fx_scale is 0
+ * goes in by fp32 atomics into grid_grad instead (the renderer zeroes the
+ * coarse levels', FusedMLRenderer.bin_f32_levels).
+ * fx_mode 5: fx_mode 4 with levels 0-7 by fp32 atomics whatever their scale
+ * (the walk's even streams compiled without page code; round 6).            */
 int rn_grid_fx_fold(const uint32_t* level_offset, const uint32_t* level_hsize,
                     const uint32_t* level_res, int32_t* fx_acc, const float* fx_scale_cur,
                     float* fx_scale_next, uint32_t* fx_vmax, int32_t* fx_redo, float* grid_grad,
