@@ -534,7 +534,9 @@ __device__ __forceinline__ void walk2_issue(Walk2& W, int s, uint32_t cnt,
             W.offB = off;
             W.oldB = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(lo, G.lo, (int)off, 0, 0);
         } else {
-            if (GM == 2 || BIN) {                        // fp32 level: still tracked
+            // fp32 level: still tracked (not GM 5's even streams: the host
+            // zeroes those levels' scales every step, so their maxima are unused)
+            if (GM == 2 || (BIN && !F32S)) {
                 const uint32_t ab = v & 0x7fffffffu;
                 if (odd) W.vmB = max(W.vmB, ab); else W.vmA = max(W.vmA, ab);
             }

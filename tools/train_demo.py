@@ -57,8 +57,11 @@ def run(steps, B, K, grid_fx, dev, scale=0.5):
     # $FX_F32_LEVELS="4,5,6,7,8": those levels by fp32 atomics (fused.fx_f32_levels)
     tr.renderer.fx_f32_levels = tuple(int(x) for x in os.environ.get("FX_F32_LEVELS", "").split(",")
                                       if x)
+    # $BIN_F32_LEVELS=n: the binned form's fp32 coarse levels (default: the renderer's)
+    if os.environ.get("BIN_F32_LEVELS"):
+        tr.renderer.bin_f32_levels = int(os.environ["BIN_F32_LEVELS"])
     gen = torch.Generator(device=dev)
-    gen.manual_seed(1234)
+    gen.manual_seed(int(os.environ.get("DEMO_SEED", 1234)))
     curve, redo_steps = [], 0
     acc_rgb, n_acc = 0.0, 0
     tail, tail_n = 0.0, 0                # the last 200 steps' mean rgb loss
