@@ -39,3 +39,22 @@ def test_cascades_and_buffers_like_reference():
     assert g.type == "ray" and g.out_dim == 4
     g.freeze_dict()
     assert not any(p.requires_grad for p in g.parameters())
+
+
+def test_binned_coarse_levels_default_by_shape():
+    """Round 6: the binned form (scale 16) sends the coarse levels by fp32
+    atomics -- 9 with K >= 8 sub-NeRFs, 8 otherwise (profiles/r06/bin_f32/);
+    scale 0.5 (the int32 atomic form) bins nothing.  The level cut of the
+    data-parallel fold stays in [0, 15]."""
+    import torch
+    from radnerf_amd.fused import FusedMLRenderer, clamp_split
+    from radnerf_amd.networks import MNGP, Ray_Gate
+    cpu = torch.device("cpu")
+    for scale, K, B, want_bin, want_n in ((16.0, 8, 1024, True, 9), (16.0, 4, 1024, True, 8),
+                                          (16.0, 2, 1024, True, 8), (0.5, 2, 8192, False, 0),
+                                          (16.0, 1, 512, False, 0)):
+        r = FusedMLRenderer(MNGP(scale, size=K, seed=3), Ray_Gate(K, seed=4), B, device=cpu,
+                            capacity=1024)
+        assert (r.grid_bin, r.bin_f32_levels) == (want_bin, want_n), (scale, K, B)
+        assert r.fx_f32_levels == ()
+    assert clamp_split(16) == 15
