@@ -144,8 +144,10 @@ def parse():
     ap.add_argument("--balance-chunks", type=int, default=None,
                     help="merged backward: 1 = big chunks a multiple of the persistent "
                          "blocks in number (the renderer's default), 0 = max_chunk each")
-    ap.add_argument("--head-chunk", type=int, default=0,
-                    help="merged passes: first chunk per block (0 = none)")
+    ap.add_argument("--head-chunk", type=int, default=None,
+                    help="merged backward: the blocks' first chunks ramp from ~0 to this many "
+                         "merged samples (0 = none; default: the renderer's, max_chunk at "
+                         "scale 0.5)")
     ap.add_argument("--pinned", action="store_true",
                     help="sub-NeRF-per-GPU layout (SURVEY.md §8(e) C5): rank r renders ALL rays "
                          "for its K/N sub-NeRFs, per-ray outputs all-gathered (strong scaling)")
@@ -329,7 +331,8 @@ def main():
         r.level_fwd = bool(args.level_fwd)
     if args.max_chunk:
         r.max_chunk = args.max_chunk
-    r.head_chunk = args.head_chunk
+    if args.head_chunk is not None:
+        r.head_chunk = args.head_chunk
     if args.min_chunk:
         r.min_chunk = args.min_chunk
     if args.enc_blocks:

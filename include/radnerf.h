@@ -209,8 +209,10 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * on one ray share atomic requests.
  * rn_bwd_plan builds the merged order (mstart [n_rays + 1] i32, perm [total]
  * i32) and the chunk schedule (chunk_first [cap_chunks + 1] i32: head_chunks
- * chunks of head_size merged samples (one per block, so the first scatter
- * starts early), then big chunks up to 7/8 of the work, then min_chunk;
+ * chunks ramping from ~0 to head_size merged samples, chunk c of
+ * [head_size c (c + 1) / (2 head_chunks), head_size (c + 1) (c + 2) / (2
+ * head_chunks)) (one per block, so the blocks' walks start staggered; none
+ * when the ramp passes 7/8 of the work), then big chunks up to 7/8 of the work, then min_chunk;
  * the big chunks are max_chunk merged samples, or with balance_blocks > 0 a
  * multiple of balance_blocks in number, each of at most max_chunk (every
  * persistent block takes the same number of them);

@@ -2391,24 +2391,36 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
 // max_samples samples (possibly none).
 struct ChunkPlan {
     int head_n, head, max_chunk, min_chunk, c1, n;
+    // first merged position of head chunk c (c <= head_n): head chunk c holds
+    // ~head (c + 1) / head_n positions, a ramp from ~0 to head
+    __host__ __device__ int hbound(int c) const {
+        return head_n > 0 ? (int)(((int64_t)head * c * (c + 1)) / (2 * (int64_t)head_n)) : 0;
+    }
     __host__ __device__ int bound(int c) const {
-        const int H = head_n * head;
-        if (c < head_n) return c * head;
+        const int H = hbound(head_n);
+        if (c < head_n) return hbound(c);
         if (c <= c1) return H + (c - head_n) * max_chunk;
         return H + (c1 - head_n) * max_chunk + (c - c1) * min_chunk;
     }
 };
 
-// head_n chunks of `head` samples first (one per block: the scatter, and so the
-// atomics, start after a short MLP phase instead of a full chunk's), then
+// head_n chunks ramping from ~0 to `head` samples first (one per block): the
+// blocks' first MLP phases end at staggered times, so the walks' requests
+// reach the memory-side atomic units spread out instead of all at once after
+// one full chunk's MLP phase, and the blocks stay out of phase after.  A ramp
+// to max_chunk: C3 1183.4 -> 1189.2 M samples/s (field_bwd 2.995 -> 2.973
+// ms), C2 853.7 -> 862.3; head chunks of one size (rounds 2 and 5) changed
+// nothing, and at scale 16 a ramp to max_chunk / 2 lost 2-5 % (the big chunks,
+// only ~2 per block there, get shorter); profiles/r06/headramp/.  Then
 // max_chunk up to 7/8 of the work, then min_chunk
 __host__ __device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head,
                                                          int max_chunk, int min_chunk, int blocks) {
     ChunkPlan p;
     p.head = head; p.max_chunk = max_chunk; p.min_chunk = min_chunk;
     const int main_end = total - total / 8;
-    p.head_n = head > 0 ? min(head_n, main_end / head) : 0;
-    const int H = p.head_n * head;
+    // the ramp takes ~head (head_n + 1) / 2 positions: none if that is past 7/8
+    p.head_n = head > 0 && (int64_t)head * (head_n + 1) / 2 <= main_end ? head_n : 0;
+    const int H = p.hbound(p.head_n);
     if (blocks > 0 && main_end > H) {
         const int64_t main = main_end - H, per = (int64_t)blocks * max_chunk;
         const int64_t m = (main + per - 1) / per;

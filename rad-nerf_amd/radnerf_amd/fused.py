@@ -308,10 +308,16 @@ class FusedMLRenderer:
         # cost of those levels' reproducibility (bench.py
         # --fx-f32-levels)
         self.fx_f32_levels = ()
-        # optional short first chunk per block (starts the scatter sooner):
-        # measured no effect on C3 (0 / 128 / 256 / 512: 3.78-3.81 ms); round 5
-        # again: C3 1185-1187 and C5 732-736 at 0-512 (profiles/r05/chunk5/)
-        self.head_chunk = 0
+        # head chunks: the first chunk of each block ramps from ~0 to
+        # head_chunk merged samples (rn_bwd_plan), so the blocks' walks start
+        # staggered instead of all after one full MLP phase.  Round 6
+        # (profiles/r06/headramp/, interleaved): a ramp to max_chunk at scale
+        # 0.5, C3 1183.4 -> 1189.2 M samples/s, C2 853.7 -> 862.3, C1 within
+        # noise (then 256); at scale 16 a ramp to max_chunk / 2 cost C4 650 ->
+        # 617 and C5 773 -> 762 (only ~2 big chunks per block, which get
+        # shorter), so none there.  (Head chunks of one size, rounds 2 and 5,
+        # changed nothing.)
+        self.head_chunk = self.max_chunk if float(model.scale) <= 0.5 and rk > 1024 else 0
         # big chunks a multiple of the persistent blocks in number (rn_bwd_plan
         # balance_blocks): every block takes the same number of them
         self.balance_chunks = True

@@ -334,18 +334,20 @@ def test_merged_backward_matches_per_model(cuda, B, K, scale):
 
 
 def test_merged_backward_chunking(cuda):
-    """Small chunks (many queue grabs, single-ray chunks above max_chunk) give
-    the same gradients."""
+    """Small chunks (many queue grabs, single-ray chunks above max_chunk) and
+    ramps of head chunks give the same gradients."""
     B, K = 2048, 2
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K)
     r = get_renderer(m, g, B)
     res = []
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)    # fp32 step (fx scales)
-    for mc, blocks in ((1024, 256), (4096, 256), (64, 37), (300, 3)):
-        r.max_chunk, r.merged_blocks = mc, blocks
+    head0 = r.head_chunk
+    for mc, blocks, head in ((1024, 256, 0), (4096, 256, 0), (64, 37, 0), (300, 3, 0),
+                             (1024, 256, 1024), (1536, 37, 900)):
+        r.max_chunk, r.merged_blocks, r.head_chunk = mc, blocks, head
         _, gr = _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, 0.0)
         res.append(gr)
-    r.max_chunk, r.merged_blocks = 1024, 256
+    r.max_chunk, r.merged_blocks, r.head_chunk = 1024, 256, head0
     # other chunkings cut the walks' records elsewhere, so the fixed-point
     # rounding of the hashed levels differs (FX_LEVEL_TOL); MLP / gate: order only
     for other in res[1:]:
@@ -356,11 +358,15 @@ def test_merged_backward_chunking(cuda):
 
 def _chunk_bounds(total, head_n, head, max_chunk, min_chunk, blocks):
     """host restatement of field.hip chunk_plan: the merged-position bound of
-    every chunk (head chunks, big chunks over 7/8 of the work -- with blocks >
-    0 a multiple of blocks in number, each <= max_chunk -- then min_chunk)"""
+    every chunk (head chunks ramping from ~0 to head, big chunks over 7/8 of
+    the work -- with blocks > 0 a multiple of blocks in number, each <=
+    max_chunk -- then min_chunk)"""
     main_end = total - total // 8
-    head_n = min(head_n, main_end // head) if head > 0 else 0
-    H = head_n * head
+    head_n = head_n if head > 0 and head * (head_n + 1) // 2 <= main_end else 0
+
+    def hbound(c):
+        return (head * c * (c + 1)) // (2 * head_n) if head_n else 0
+    H = hbound(head_n)
     big, mm = max_chunk, 0
     if blocks > 0 and main_end > H:
         per = blocks * max_chunk
@@ -370,7 +376,7 @@ def _chunk_bounds(total, head_n, head, max_chunk, min_chunk, blocks):
 
     def bound(c):
         if c < head_n:
-            return c * head
+            return hbound(c)
         if c <= c1:
             return H + (c - head_n) * big
         return H + (c1 - head_n) * big + (c - c1) * min_chunk
@@ -379,19 +385,26 @@ def _chunk_bounds(total, head_n, head, max_chunk, min_chunk, blocks):
     return [bound(c) for c in range(n)], c1 - head_n, big, mm
 
 
-@pytest.mark.parametrize("B,K,scale,mc,bal", [(2048, 2, 0.5, 1536, 256), (1024, 4, 16.0, 4096, 256),
-                                              (1024, 8, 16.0, 8192, 256), (2048, 2, 0.5, 1536, 0),
-                                              (512, 4, 16.0, 2560, 37)])
-def test_chunk_schedule(cuda, B, K, scale, mc, bal):
+@pytest.mark.parametrize("B,K,scale,mc,bal,head", [(2048, 2, 0.5, 1536, 256, None),
+                                                   (1024, 4, 16.0, 4096, 256, None),
+                                                   (1024, 8, 16.0, 8192, 256, None),
+                                                   (2048, 2, 0.5, 1536, 0, 0),
+                                                   (512, 4, 16.0, 2560, 37, 2560),
+                                                   (4096, 2, 0.5, 1024, 256, 700)])
+def test_chunk_schedule(cuda, B, K, scale, mc, bal, head):
     """rn_bwd_plan's chunk list against the host restatement of its schedule:
     every chunk starts at the first ray whose merged start reaches its bound,
     the count is the plan's; balanced (balance_blocks > 0), no block has more
     big chunks to take than the others (C4 at 2560 left a few blocks one big
-    chunk behind the rest)."""
+    chunk behind the rest).  head: the ramp of head chunks (None: the
+    renderer's default, a ramp to max_chunk at scale 0.5)."""
     m, g, o, d, noise, seeds, bits = _setup(cuda, B=B, K=K, scale=scale)
     esf = 1.0 / 256 if scale > 0.5 else 0.0
     r = get_renderer(m, g, B)
+    head0 = r.head_chunk
     r.max_chunk, r.balance_chunks = mc, bal > 0
+    if head is not None:
+        r.head_chunk = head
     if bal:
         r.merged_blocks = bal
     _run(ml_render_fused, m, g, o, d, noise, seeds, cuda, esf)
@@ -400,7 +413,9 @@ def test_chunk_schedule(cuda, B, K, scale, mc, bal):
     torch.cuda.synchronize()
     ms = w.mstart[:B + 1].cpu().numpy().astype(np.int64)
     total = int(ms[B])
-    bounds, n_big, big, per_block = _chunk_bounds(total, 0, 0, mc, min(r.min_chunk, mc), bal)
+    head_n = r.merged_blocks if r.head_chunk else 0
+    bounds, n_big, big, per_block = _chunk_bounds(total, head_n, min(r.head_chunk, mc), mc,
+                                                  min(r.min_chunk, mc), bal)
     n = int(w.queue[1])
     assert n == len(bounds)
     first = r._chunks[:n + 1].cpu().numpy()
@@ -410,7 +425,7 @@ def test_chunk_schedule(cuda, B, K, scale, mc, bal):
         # at most per_block big chunks for every block, and nearly all take
         # that many (floor division leaves at most a few a chunk short)
         assert bal * (per_block - 1) < n_big <= bal * per_block and big <= mc, (n_big, big)
-    r.max_chunk, r.merged_blocks, r.balance_chunks = mc, 256, True
+    r.max_chunk, r.merged_blocks, r.balance_chunks, r.head_chunk = mc, 256, True, head0
     assert all(torch.isfinite(x).all() for x in gr)
 
 
