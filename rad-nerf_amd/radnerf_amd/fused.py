@@ -299,7 +299,22 @@ class FusedMLRenderer:
         # initial pool: records per (ray, sub-NeRF) at scale 16 (C5's replay:
         # 63.5 records x 95 samples; tools/records_sim.py), x 1.15
         self.bin_records_per_pair = 6912
+        # the tail's chunks (the last 1/8 of the merged positions): small
+        # enough for the blocks to finish together, large enough that a
+        # chunk's fixed cost -- K model switches (weights, parked dW) and ring
+        # flushes -- stays small.  Round 6, interleaved (profiles/r06/minchunk/):
+        # C3 256 1182, 384 1189, 512 1188, 768 1179; C5 512 774, 1024 782,
+        # 2048 780, 3072 789, 3584 786, 4096 781; C4 512 649, 640 648, 768 642,
+        # 1024 651.5, 2048 623; the pinned rank 512 581, 1024 578, 2048 578.
+        # (At C5 3072 leaves ~250 tail chunks, at most one per block; the
+        # optimum moves with the step's size, so the rule holds from the
+        # measured ray counts up.)
         self.min_chunk = 512
+        if float(model.scale) > 0.5:
+            if model.size >= 8 and n_rays >= 8192:
+                self.min_chunk = 3072
+            elif model.size >= 4 and n_rays >= 4096:
+                self.min_chunk = 1024
         # hash levels whose grid gradient goes in by fp32 atomics instead of
         # fixed point (int32 or binned): () = none, every level an exact
         # integer sum (bitwise reproducible).  (3, ..., 8) at C3 brings the

@@ -18,7 +18,7 @@ def test_chunk_count_within_documented_cap():
     worst = 0.0
     for _ in range(3000):
         max_chunk = int(rng.choice([256, 512, 1024, 1536, 2560, 4096, 8192, 12288]))
-        min_chunk = int(rng.choice([256, 512])) if max_chunk >= 512 else 256
+        min_chunk = int(rng.choice([256, 512, 1024, 3072])) if max_chunk >= 512 else 256
         min_chunk = min(min_chunk, max_chunk)
         blocks = int(rng.choice([0, 37, 128, 256]))
         head = int(rng.choice([0, 256, 512]))
