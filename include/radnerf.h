@@ -212,7 +212,8 @@ int rn_field_bwd(const float* xyzs, const float* dirs, int64_t n_samples, const 
  * chunks ramping from ~0 to head_size merged samples, chunk c of
  * [head_size c (c + 1) / (2 head_chunks), head_size (c + 1) (c + 2) / (2
  * head_chunks)) (one per block, so the blocks' walks start staggered; none
- * when the ramp passes 7/8 of the work), then big chunks up to 7/8 of the work, then min_chunk;
+ * when the ramp passes 15/16 of the work), then big chunks up to 15/16 of the work, then
+ * min_chunk;
  * the big chunks are max_chunk merged samples, or with balance_blocks > 0 a
  * multiple of balance_blocks in number, each of at most max_chunk (every
  * persistent block takes the same number of them);

@@ -2379,7 +2379,7 @@ k_bwd_plan_multi(int B, int K, const int32_t* __restrict__ counts,
 }
 
 // Chunk schedule of the merged backward over the merged positions [0, total):
-// big chunks for the first 7/8 of the work, then chunks of min_chunk (a short
+// big chunks for the first 15/16 of the work, then chunks of min_chunk (a short
 // tail: blocks finish together).  With `blocks` > 0 the big chunks are a
 // multiple of the persistent blocks in number, each <= max_chunk positions
 // (size ceil(main / (blocks m)), m = ceil(main / (blocks max_chunk))): every
@@ -2412,13 +2412,18 @@ struct ChunkPlan {
 // ms), C2 853.7 -> 862.3; head chunks of one size (rounds 2 and 5) changed
 // nothing, and at scale 16 a ramp to max_chunk / 2 lost 2-5 % (the big chunks,
 // only ~2 per block there, get shorter); profiles/r06/headramp/.  Then
-// max_chunk up to 7/8 of the work, then min_chunk
+// max_chunk up to 15/16 of the work, then min_chunk (round 6: a tail of 1/16
+// instead of 1/8, with its chunks sized by shape on the host: C3 1191 -> 1194,
+// C4 653 -> 658, C5 789 -> 791; no tail at all lost 1 %; profiles/r06/tail/)
 __host__ __device__ __forceinline__ ChunkPlan chunk_plan(int total, int head_n, int head,
                                                          int max_chunk, int min_chunk, int blocks) {
     ChunkPlan p;
     p.head = head; p.max_chunk = max_chunk; p.min_chunk = min_chunk;
-    const int main_end = total - total / 8;
-    // the ramp takes ~head (head_n + 1) / 2 positions: none if that is past 7/8
+#ifndef RN_TAIL_SHIFT              // (timing studies: -D overrides the tail's share, 2^-shift)
+#define RN_TAIL_SHIFT 4
+#endif
+    const int main_end = total - (RN_TAIL_SHIFT < 31 ? total >> RN_TAIL_SHIFT : 0);
+    // the ramp takes ~head (head_n + 1) / 2 positions: none if that is past the main part
     p.head_n = head > 0 && (int64_t)head * (head_n + 1) / 2 <= main_end ? head_n : 0;
     const int H = p.hbound(p.head_n);
     if (blocks > 0 && main_end > H) {

@@ -299,7 +299,8 @@ class FusedMLRenderer:
         # initial pool: records per (ray, sub-NeRF) at scale 16 (C5's replay:
         # 63.5 records x 95 samples; tools/records_sim.py), x 1.15
         self.bin_records_per_pair = 6912
-        # the tail's chunks (the last 1/8 of the merged positions): small
+        # the tail's chunks (the last 1/16 of the merged positions; 1/8 until
+        # late round 6, where these sweeps ran): small
         # enough for the blocks to finish together, large enough that a
         # chunk's fixed cost -- K model switches (weights, parked dW) and ring
         # flushes -- stays small.  Round 6, interleaved (profiles/r06/minchunk/):
@@ -312,9 +313,9 @@ class FusedMLRenderer:
         self.min_chunk = 512
         if float(model.scale) > 0.5:
             if model.size >= 8 and n_rays >= 8192:
-                self.min_chunk = 3072
-            elif model.size >= 4 and n_rays >= 4096:
-                self.min_chunk = 1024
+                # with the 1/16 tail: 1536 791 vs 3072 784 (profiles/r06/tail/)
+                self.min_chunk = 1536
+            # (K = 4: 1024 won with the 1/8 tail; with 1/16, 512: 658 vs 653)
         # hash levels whose grid gradient goes in by fp32 atomics instead of
         # fixed point (int32 or binned): () = none, every level an exact
         # integer sum (bitwise reproducible).  (3, ..., 8) at C3 brings the

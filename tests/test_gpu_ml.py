@@ -358,10 +358,10 @@ def test_merged_backward_chunking(cuda):
 
 def _chunk_bounds(total, head_n, head, max_chunk, min_chunk, blocks):
     """host restatement of field.hip chunk_plan: the merged-position bound of
-    every chunk (head chunks ramping from ~0 to head, big chunks over 7/8 of
+    every chunk (head chunks ramping from ~0 to head, big chunks over 15/16 of
     the work -- with blocks > 0 a multiple of blocks in number, each <=
     max_chunk -- then min_chunk)"""
-    main_end = total - total // 8
+    main_end = total - total // 16
     head_n = head_n if head > 0 and head * (head_n + 1) // 2 <= main_end else 0
 
     def hbound(c):

@@ -63,16 +63,16 @@ def test_binned_coarse_levels_default_by_shape():
 def test_chunk_defaults_by_shape():
     """Round 6's measured chunk defaults (fused.FusedMLRenderer; profiles/r06/
     headramp/, minchunk/): head chunks ramp to max_chunk at scale 0.5 above
-    1024 ray x sub-NeRF pairs, none at scale 16; the tail's chunks are 3072
-    merged samples at K >= 8 (8192+ rays) and 1024 at K = 4 (4096+ rays) at
-    scale 16, 512 otherwise."""
+    1024 ray x sub-NeRF pairs, none at scale 16; the tail's chunks (the last
+    1/16 of the merged positions) are 1536 merged samples at K >= 8 (8192+
+    rays) at scale 16, 512 otherwise."""
     import torch
     from radnerf_amd.fused import FusedMLRenderer
     from radnerf_amd.networks import MNGP, Ray_Gate
     cpu = torch.device("cpu")
     for scale, K, B, head, mn in ((0.5, 2, 8192, 1536, 512), (0.5, 1, 8192, 1024, 512),
-                                  (0.5, 1, 1024, 0, 512), (16.0, 8, 8192, 0, 3072),
-                                  (16.0, 4, 4096, 0, 1024), (16.0, 8, 4096, 0, 1024),
+                                  (0.5, 1, 1024, 0, 512), (16.0, 8, 8192, 0, 1536),
+                                  (16.0, 4, 4096, 0, 512), (16.0, 8, 4096, 0, 512),
                                   (16.0, 1, 65536, 0, 512)):
         r = FusedMLRenderer(MNGP(scale, size=K, seed=3), Ray_Gate(K, seed=4), B, device=cpu,
                             capacity=1024)
